@@ -1,0 +1,316 @@
+#!/usr/bin/env python3
+"""make_golden.py -- regenerates the committed golden fixtures (dev container only).
+
+TEST INFRASTRUCTURE.  Needs /root/reference (the reference sources) and the
+reference libraries built by `make -C oracle ref`.  The fixtures it writes are
+plain data (inputs + expected codes); nothing from the reference is copied.
+
+Where expected codes come from
+  * code_avx512: the reference fd_ed25519_verify compiled with FD_HAS_AVX512
+    (oracle/_ref/libfdref_avx512.so) -- the backend the reference's
+    config/machine/native.mk picks on an AVX-512-IFMA host and the CPU path
+    bench.py times.  This is THE golden code.
+  * code_ref: the same sources compiled for the portable `ref` backend.
+    Recorded for information (the two differ on pubkey-decode failures,
+    SURVEY.md §8(a) A4/A5).
+  * ok: the accept/reject the reference's own test files assert
+    (test_ed25519_wycheproof.c / test_ed25519_cctv.c `.ok`, the two
+    malleability .bin files); -1 where the reference tests say nothing.
+
+Files written (tests/golden/):
+  vectors_ref.bin   Wycheproof (set 1), CCTV (set 2), malleability fail/pass (sets 4/5)
+  synthetic.bin     config-1 valid sigs (set 10), adversarial classes (sets 20..39),
+                    variable-length messages 0..1232 B (set 11)
+  txn_batches.bin   multi-signature single-message batches (A2 precedence)
+  sha512_kat.bin    SHA-512 known answers (fd_sha512_test_vector.c + CAVP ShortMsg/LongMsg)
+
+Record format (ed25519 files), little endian:
+  u32 set, u32 tc_id, i8 code_avx512, i8 code_ref, i8 ok, u8 0, u32 msg_sz,
+  u8 sig[64], u8 pub[32], u8 msg[msg_sz]
+txn_batches.bin record:
+  u32 n, u32 msg_sz, i8 code_avx512, i8 code_ref, u16 0, u8 sigs[64n], u8 pubs[32n], u8 msg[msg_sz]
+sha512_kat.bin record:
+  u32 msg_sz, u8 digest[64], u8 msg[msg_sz]
+"""
+import ctypes
+import os
+import struct
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_SRC = os.environ.get("FD_REF_SRC", "/root/reference/src")
+
+P = 2**255 - 19
+L = 2**252 + 27742317777372353535851937790883648493
+# y coordinates of the order-8 points, as listed in src/ballet/ed25519/fd_curve25519.h:86-93
+Y0 = int.from_bytes(bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05"), "little")
+Y1 = int.from_bytes(bytes.fromhex("c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a"), "little")
+
+
+def load_libs():
+    libs = {}
+    for b in ("avx512", "ref"):
+        lib = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "libfdref_%s.so" % b))
+        lib.fdref_verify.restype = ctypes.c_int
+        lib.fdref_verify.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
+        lib.fdref_verify_batch_single_msg.restype = ctypes.c_int
+        lib.fdref_verify_batch_single_msg.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p,
+                                                      ctypes.c_char_p, ctypes.c_ulong]
+        lib.fdref_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
+        lib.fdref_public_from_private.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        assert lib.fdref_backend_avx512() == (1 if b == "avx512" else 0)
+        libs[b] = lib
+    return libs
+
+
+LIBS = None
+
+
+def verify(msg, sig, pub):
+    return tuple(LIBS[b].fdref_verify(msg, len(msg), sig, pub) for b in ("avx512", "ref"))
+
+
+def verify_batch(msg, sigs, pubs, n):
+    return tuple(LIBS[b].fdref_verify_batch_single_msg(msg, len(msg), sigs, pubs, n) for b in ("avx512", "ref"))
+
+
+def keypair(rng):
+    priv = rng.bytes(32)
+    pub = ctypes.create_string_buffer(32)
+    LIBS["avx512"].fdref_public_from_private(pub, priv)
+    return priv, pub.raw
+
+
+def sign(msg, pub, priv):
+    sig = ctypes.create_string_buffer(64)
+    LIBS["avx512"].fdref_sign(sig, msg, len(msg), pub, priv)
+    return sig.raw
+
+
+def rec(set_id, tc_id, codes, ok, msg, sig, pub):
+    assert len(sig) == 64 and len(pub) == 32
+    return struct.pack("<IIbbbBI", set_id, tc_id, codes[0], codes[1], ok, 0, len(msg)) + sig + pub + msg
+
+
+def enc(y, sign_bit):
+    return (y | (sign_bit << 255)).to_bytes(32, "little")
+
+
+def extract_reference_vectors():
+    exe = "/tmp/fdgpu_extract_vectors"
+    out = "/tmp/fdgpu_vectors.bin"
+    cmd = ["gcc", "-std=c17", "-O1", "-w", "-I" + REF_SRC, "-DFD_HAS_HOSTED=1", "-D_XOPEN_SOURCE=700",
+           "-DFD_HAS_INT128=1", "-DFD_HAS_DOUBLE=1", "-DFD_HAS_X86=1", "-DFD_HAS_SSE=1", "-DFD_HAS_AVX=1",
+           "-o", exe, os.path.join(HERE, "extract_vectors.c")]
+    subprocess.check_call(cmd)
+    subprocess.check_call([exe, out])
+    data = open(out, "rb").read()
+    vecs, off = [], 0
+    while off < len(data):
+        set_id, tc_id, ok, msg_sz = struct.unpack_from("<IIiI", data, off)
+        off += 16
+        sig = data[off:off + 64]; pub = data[off + 64:off + 96]; off += 96
+        msg = data[off:off + msg_sz]; off += msg_sz
+        vecs.append((set_id, tc_id, ok, msg, sig, pub))
+    return vecs
+
+
+def gen_vectors_ref(vecs):
+    out = []
+    for set_id, tc_id, ok, msg, sig, pub in vecs:
+        if set_id in (1, 2):
+            out.append(rec(set_id, tc_id, verify(msg, sig, pub), ok, msg, sig, pub))
+    # malleability records: 96-byte {sig, pub}, msg "Zcash"
+    # (src/ballet/ed25519/test_ed25519_signature_malleability.c:4-15,21)
+    for set_id, fname, ok in ((4, "should_fail", 0), (5, "should_pass", 1)):
+        path = os.path.join(REF_SRC, "ballet/ed25519/test_ed25519_signature_malleability_%s.bin" % fname)
+        raw = open(path, "rb").read()
+        assert len(raw) % 96 == 0
+        for i in range(len(raw) // 96):
+            sig = raw[96 * i:96 * i + 64]; pub = raw[96 * i + 64:96 * i + 96]
+            out.append(rec(set_id, i, verify(b"Zcash", sig, pub), ok, b"Zcash", sig, pub))
+    return out
+
+
+def gen_synthetic():
+    rng = np.random.default_rng(1234)
+    out = []
+    # set 10: config 1 -- 1024 distinct keys, 200-byte random messages, all valid
+    keys = [keypair(rng) for _ in range(1024)]
+    for i, (priv, pub) in enumerate(keys):
+        msg = rng.bytes(200)
+        sig = sign(msg, pub, priv)
+        c = verify(msg, sig, pub)
+        assert c == (0, 0)
+        out.append(rec(10, i, c, 1, msg, sig, pub))
+    # set 11: config 3 shape -- message length uniform in 0..1232 (MTU), all valid
+    for i in range(256):
+        priv, pub = keys[i]
+        msg = rng.bytes(int(rng.integers(0, 1233)))
+        sig = sign(msg, pub, priv)
+        c = verify(msg, sig, pub)
+        assert c == (0, 0)
+        out.append(rec(11, i, c, 1, msg, sig, pub))
+    # explicit SHA block-boundary lengths: 64+msg+17 crosses 128*k
+    for j, m in enumerate([0, 1, 46, 47, 48, 63, 64, 110, 111, 112, 127, 128, 175, 176, 239, 240, 1231, 1232]):
+        priv, pub = keys[j]
+        msg = rng.bytes(m)
+        sig = sign(msg, pub, priv)
+        out.append(rec(12, j, verify(msg, sig, pub), 1, msg, sig, pub))
+
+    def base(i, n=200):
+        priv, pub = keys[i % len(keys)]
+        msg = rng.bytes(n)
+        return msg, sign(msg, pub, priv), pub, priv
+
+    tc = 0
+
+    def add(set_id, msg, sig, pub, ok=-1):
+        nonlocal tc
+        out.append(rec(set_id, tc, verify(msg, sig, pub), ok, msg, sig, pub))
+        tc += 1
+
+    for i in range(64):   # set 20: 1-bit flip in the message -> ERR_MSG
+        msg, sig, pub, _ = base(i)
+        b = bytearray(msg); b[i % len(b)] ^= 1 << (i % 8)
+        add(20, bytes(b), sig, pub, 0)
+    for i in range(64):   # set 21: 1-bit flip in S low bytes
+        msg, sig, pub, _ = base(i)
+        s = bytearray(sig); s[32 + (i % 16)] ^= 1 << (i % 8)
+        add(21, msg, bytes(s), pub, 0)
+    for i in range(32):   # set 22: S >= L via the high byte -> ERR_SIG
+        msg, sig, pub, _ = base(i)
+        s = bytearray(sig); s[63] |= (0x10, 0x20, 0x40, 0x80)[i % 4]
+        add(22, msg, bytes(s), pub, 0)
+    for i, S in enumerate([L, L - 1, L + 1, 2**256 - 1, 2**253, 0, 1]):   # set 23: scalar boundaries
+        msg, sig, pub, _ = base(i)
+        add(23, msg, sig[:32] + S.to_bytes(32, "little"), pub, -1)
+    for i in range(128):  # set 24: random pubkey bytes (about half do not decode)
+        msg, sig, _, _ = base(i)
+        add(24, msg, sig, rng.bytes(32), 0)
+    for i in range(128):  # set 25: random R bytes
+        msg, sig, pub, _ = base(i)
+        add(25, msg, rng.bytes(32) + sig[32:], pub, 0)
+    # set 26/27: x=0 encodings with sign bit 1 (y = 1, y = p-1) as A / as R
+    for i, y in enumerate([1, P - 1, P + 1]):
+        for sgn in (0, 1):
+            msg, sig, pub, _ = base(i)
+            add(26, msg, sig, enc(y, sgn), 0)
+            add(27, msg, enc(y, sgn) + sig[32:], pub, 0)
+    # set 28/29: non-canonical y = p + v, v in [0, 18], both signs, as A / as R
+    for v in range(19):
+        for sgn in (0, 1):
+            msg, sig, pub, _ = base(v)
+            add(28, msg, sig, enc(P + v, sgn), 0)
+            add(29, msg, enc(P + v, sgn) + sig[32:], pub, 0)
+    # set 30/31: the small-order y's (0, 1, p-1, y0, y1) and their +p aliases, both signs
+    for y in (0, 1, P - 1, Y0, Y1, P, P + 1):
+        for sgn in (0, 1):
+            if y >= 2**255:
+                continue
+            msg, sig, pub, _ = base(y & 0xff)
+            add(30, msg, sig, enc(y, sgn), 0)
+            add(31, msg, enc(y, sgn) + sig[32:], pub, 0)
+    # set 32: small-order A with a signature made to verify against it is impossible
+    # without the private key; instead mixed-order A = A_valid + T (torsion): sign
+    # with the honest key, publish the torsioned key -> equation fails (cofactorless)
+    # Covered by CCTV; here random full-order A with R swapped between two valid sigs.
+    for i in range(32):
+        msg, sig, pub, _ = base(i)
+        msg2, sig2, pub2, _ = base(i + 1)
+        add(32, msg, sig2[:32] + sig[32:], pub, 0)
+    # set 33: empty and single-byte messages, valid
+    for i, n in enumerate([0, 1, 2, 3]):
+        msg, sig, pub, _ = base(i, n)
+        add(33, msg, sig, pub, 1)
+    return out
+
+
+def gen_txn_batches():
+    rng = np.random.default_rng(4321)
+    keys = [keypair(rng) for _ in range(64)]
+    out = []
+
+    def one(n, corrupt):
+        msg = rng.bytes(int(rng.integers(0, 600)))
+        sigs, pubs = [], []
+        for j in range(max(n, 1)):
+            priv, pub = keys[int(rng.integers(0, len(keys)))]
+            sig = sign(msg, pub, priv)
+            kind = corrupt.get(j)
+            if kind == "msg":       # wrong signature (other message) -> -3 in phase 2
+                sig = sign(msg + b"x", pub, priv)
+            elif kind == "S":       # S >= L -> -1 in phase 1
+                sig = sig[:63] + bytes([sig[63] | 0xf0])
+            elif kind == "A_small":  # small-order A -> -2 in phase 1
+                pub = enc(0, 0)
+            elif kind == "A_bad":   # undecodable A (y=2: u=3,v=4d+1 non-square) -> -1 avx512 / -2 ref
+                pub = enc(2, 0)
+            elif kind == "R_small":  # small-order R -> -1
+                sig = enc(1, 0) + sig[32:]
+            sigs.append(sig); pubs.append(pub)
+        sigs_b = b"".join(sigs[:n] if n else sigs[:0]); pubs_b = b"".join(pubs[:n] if n else pubs[:0])
+        pad_s = sigs_b if n else bytes(64); pad_p = pubs_b if n else bytes(32)
+        codes = verify_batch(msg, pad_s, pad_p, n)
+        out.append(struct.pack("<IIbbH", n, len(msg), codes[0], codes[1], 0) + sigs_b + pubs_b + msg)
+
+    kinds = ["msg", "S", "A_small", "A_bad", "R_small"]
+    for n in range(1, 13):
+        one(n, {})
+    # every ordered pair of failure kinds at two positions (probes the two-phase precedence)
+    for a in kinds:
+        for b in kinds:
+            for n in (2, 3, 5):
+                one(n, {0: a, 1: b})
+                one(n, {n - 1: a, 0: b})
+    for _ in range(64):
+        n = int(rng.integers(1, 13))
+        corrupt = {int(rng.integers(0, n)): kinds[int(rng.integers(0, len(kinds)))] for _ in range(int(rng.integers(0, 3)))}
+        one(n, corrupt)
+    one(16, {})
+    one(16, {15: "msg"})
+    one(17, {})            # n > 16 -> -1 before any work (fd_ed25519_user.c:238-240)
+    one(0, {})             # n == 0 -> -1
+    return out
+
+
+def gen_sha512(vecs):
+    out = []
+    for set_id, tc_id, ok, msg, sig, pub in vecs:
+        if set_id == 3:
+            out.append(struct.pack("<I", len(msg)) + sig + msg)
+    # NIST CAVP (src/ballet/sha512/cavp/SHA512{Short,Long}Msg.rsp), every 4th record
+    for fname in ("SHA512ShortMsg.rsp", "SHA512LongMsg.rsp"):
+        path = os.path.join(REF_SRC, "ballet/sha512/cavp", fname)
+        ln = None; msg = None; k = 0
+        for line in open(path):
+            line = line.strip()
+            if line.startswith("Len ="):
+                ln = int(line.split("=")[1])
+            elif line.startswith("Msg ="):
+                msg = bytes.fromhex(line.split("=")[1].strip())[: ln // 8]
+            elif line.startswith("MD ="):
+                md = bytes.fromhex(line.split("=")[1].strip())
+                if k % 4 == 0:
+                    out.append(struct.pack("<I", len(msg)) + md + msg)
+                k += 1
+    return out
+
+
+def main():
+    global LIBS
+    LIBS = load_libs()
+    vecs = extract_reference_vectors()
+    for name, recs in (("vectors_ref.bin", gen_vectors_ref(vecs)), ("synthetic.bin", gen_synthetic()),
+                       ("txn_batches.bin", gen_txn_batches()), ("sha512_kat.bin", gen_sha512(vecs))):
+        with open(os.path.join(HERE, name), "wb") as f:
+            f.write(b"".join(recs))
+        print(name, len(recs), "records", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

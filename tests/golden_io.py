@@ -1,0 +1,42 @@
+"""Readers for the committed golden fixtures (format: tests/golden/make_golden.py docstring)."""
+import os
+import struct
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def read_sigs(name):
+    """-> list of dict(set, tc_id, code, code_ref, ok, msg, sig, pub)."""
+    data = open(os.path.join(GOLDEN, name), "rb").read()
+    out, off = [], 0
+    while off < len(data):
+        set_id, tc_id, ca, cr, ok, _, msg_sz = struct.unpack_from("<IIbbbBI", data, off)
+        off += 16
+        sig = data[off:off + 64]; pub = data[off + 64:off + 96]; off += 96
+        msg = data[off:off + msg_sz]; off += msg_sz
+        out.append(dict(set=set_id, tc_id=tc_id, code=ca, code_ref=cr, ok=ok, msg=msg, sig=sig, pub=pub))
+    return out
+
+
+def read_txns(name="txn_batches.bin"):
+    """-> list of dict(n, code, code_ref, msg, sigs[list], pubs[list])."""
+    data = open(os.path.join(GOLDEN, name), "rb").read()
+    out, off = [], 0
+    while off < len(data):
+        n, msg_sz, ca, cr, _ = struct.unpack_from("<IIbbH", data, off)
+        off += 12
+        sigs = [data[off + 64 * j:off + 64 * j + 64] for j in range(n)]; off += 64 * n
+        pubs = [data[off + 32 * j:off + 32 * j + 32] for j in range(n)]; off += 32 * n
+        msg = data[off:off + msg_sz]; off += msg_sz
+        out.append(dict(n=n, code=ca, code_ref=cr, msg=msg, sigs=sigs, pubs=pubs))
+    return out
+
+
+def read_sha(name="sha512_kat.bin"):
+    data = open(os.path.join(GOLDEN, name), "rb").read()
+    out, off = [], 0
+    while off < len(data):
+        (sz,) = struct.unpack_from("<I", data, off); off += 4
+        md = data[off:off + 64]; off += 64
+        out.append((data[off:off + sz], md)); off += sz
+    return out
