@@ -1,0 +1,615 @@
+/* fd_ed25519_gpu.hip -- MI355X (gfx950) Ed25519 batch verifier: kernels and
+   the C ABI declared in include/fd_ed25519_gpu.h.
+
+   One signature per lane.  The verify kernel does, per lane:
+     S < l check -> decode A, R (sqrt-ratio ladder) -> small-order checks ->
+     SHA-512(R || A || M) with M streamed from HBM -> reduce mod l ->
+     signed fixed-window recoding of k (4-bit) and S (8-bit) ->
+     table of [0..8](-A) in a per-lane HBM/L2 scratch -> joint double-scalar
+     multiplication [k](-A) + [S]B with the [0..128]B affine table in LDS ->
+     projective compare against R.
+   Semantics follow fd_ed25519_verify (src/ballet/ed25519/fd_ed25519_user.c:
+   134-229) with the FD_HAS_AVX512 error mapping (SURVEY.md §8(a) A-spec).
+
+   Host side: a context owns, per device, a stream, the B table, descriptor /
+   arena / code staging buffers and the A-table scratch.  Batches are sharded
+   contiguously over the context's devices; no collective is needed (every
+   signature is independent). */
+
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+
+#include "../../include/fd_ed25519_gpu.h"
+#include "fd_f25519_dev.h"
+#include "fd_curve25519_dev.h"
+#include "fd_sha512_dev.h"
+#include "fd_scalar_dev.h"
+
+#define FD_VERIFY_BLOCK   256          /* threads per workgroup              */
+#ifndef FD_VERIFY_WAVES_PER_EU
+#define FD_VERIFY_WAVES_PER_EU 2       /* -> <= 256 VGPR+AGPR per lane       */
+#endif
+#define FD_BTAB_N         129          /* [0..128]B                          */
+#define FD_BTAB_STRIDE    32           /* u32 per entry: 3 x 10 limbs + pad  */
+#define FD_ATAB_N         9            /* [0..8](-A)                         */
+#define FD_ATAB_WORDS     40           /* u32 per entry (4 fe)               */
+
+/* ------------------------------------------------------------------ loads */
+
+/* n little-endian words starting at an arbitrary byte offset off (read
+   through aligned dwords, clamped to the readable arena). */
+template<int N>
+__device__ __forceinline__ void load_words( uint32_t out[ N ], uint8_t const * arena, uint32_t off, uint32_t lim_dw ) {
+  uint32_t const * a32 = (uint32_t const *)arena;
+  uint32_t dw = off >> 2, sh = off & 3u;
+  uint32_t prev = a32[ min( dw, lim_dw ) ];
+#pragma unroll
+  for( int i=0; i<N; i++ ) {
+    uint32_t nxt = a32[ min( dw+1u+(uint32_t)i, lim_dw ) ];
+    out[i] = __builtin_amdgcn_alignbyte( nxt, prev, sh );
+    prev = nxt;
+  }
+}
+
+/* ------------------------------------------------------------------ B table */
+
+/* Device init: lane i computes [i]B and stores its affine precomputed form
+   (Y+X, Y-X, 2dXY) into btab[i*FD_BTAB_STRIDE ...].  B decoded from its
+   standard encoding (y = 4/5, x even). */
+__global__ void fd_ed25519_btab_init( uint32_t * btab ) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= FD_BTAB_N ) return;
+  uint32_t benc[ 8 ];
+  benc[0] = 0x66666658u;
+#pragma unroll
+  for( int j=1; j<8; j++ ) benc[j] = 0x66666666u;
+  ge_p3 B; ge_decode( B, benc, true );
+  ge_precomp Bp;
+  { fe d2; fe_const_d2( d2 ); fe_add_r( Bp.YpX, B.Y, B.X ); fe_sub_r( Bp.YmX, B.Y, B.X ); fe_mul( Bp.T2d, B.T, d2 ); }
+  ge_p3 acc; ge_identity( acc );
+  for( int bit=7; bit>=0; bit-- ) {
+    ge_dbl( acc, acc, true );
+    if( (i >> bit) & 1 ) ge_madd( acc, acc, Bp, true );
+  }
+  fe zi, x, y, xy, d2, o0, o1, o2;
+  fe_invert( zi, acc.Z );
+  fe_mul( x, acc.X, zi ); fe_mul( y, acc.Y, zi );
+  fe_const_d2( d2 );
+  fe_add_r( o0, y, x ); fe_sub_r( o1, y, x ); fe_mul( xy, x, y ); fe_mul( o2, xy, d2 );
+  uint32_t * e = btab + i * FD_BTAB_STRIDE;
+  for( int j=0; j<10; j++ ) { e[j] = o0.v[j]; e[10+j] = o1.v[j]; e[20+j] = o2.v[j]; }
+  e[30] = 0u; e[31] = 0u;
+}
+
+/* ------------------------------------------------------------------ verify */
+
+struct verify_args {
+  uint8_t const *           arena;
+  uint64_t                  arena_sz;
+  fd_ed25519_desc_t const * desc;
+  uint64_t                  n;
+  int8_t *                  out;
+  uint32_t const *          btab;      /* FD_BTAB_N * FD_BTAB_STRIDE u32 */
+  uint32_t *                atab;      /* FD_ATAB_N * FD_ATAB_WORDS * stride u32 */
+  uint64_t                  atab_stride;
+  int                       ref_codes;
+};
+
+/* SHA-512(R || A || M) mod l.  R, A: 8 LE words each; message streamed. */
+__device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 ], uint32_t const Aw[ 8 ],
+                                          uint8_t const * arena, uint32_t msg_off, uint32_t msg_sz, uint32_t lim_dw ) {
+  uint64_t h[ 8 ]; sha512_init_state( h );
+  uint32_t total = 64u + msg_sz;
+  uint32_t nblk = (total + 17u + 127u) >> 7;
+  uint32_t const * a32 = (uint32_t const *)arena;
+  uint32_t sh = msg_off & 3u;
+  for( uint32_t b=0; b<nblk; b++ ) {
+    uint64_t W[ 16 ];
+#pragma unroll
+    for( int j=0; j<16; j++ ) {
+      uint32_t s = (b << 7) + 8u*(uint32_t)j;          /* stream byte offset of this word */
+      uint32_t hi, lo;                                  /* big-endian halves */
+      if( b == 0 && j < 8 ) {
+        uint32_t const * src = (j < 4) ? Rw : Aw;
+        int jj = j & 3;
+        hi = sha_bswap32( src[2*jj] ); lo = sha_bswap32( src[2*jj+1] );
+      } else {
+        int32_t m = (int32_t)(s - 64u);                 /* message byte index of the word's first byte */
+        uint32_t base = msg_off + (uint32_t)m;
+        uint32_t dw = base >> 2;
+        uint32_t d0 = a32[ min( dw,      lim_dw ) ];
+        uint32_t d1 = a32[ min( dw + 1u, lim_dw ) ];
+        uint32_t d2 = a32[ min( dw + 2u, lim_dw ) ];
+        uint32_t w0 = __builtin_amdgcn_alignbyte( d1, d0, sh );   /* bytes m..m+3 LE */
+        uint32_t w1 = __builtin_amdgcn_alignbyte( d2, d1, sh );   /* bytes m+4..m+7  */
+        hi = sha_bswap32( w0 ); lo = sha_bswap32( w1 );
+        /* padding: keep bytes < msg_sz, 0x80 at msg_sz, zeros after */
+        int32_t rem0 = (int32_t)msg_sz - m;             /* valid bytes from m   */
+        int32_t rem1 = rem0 - 4;
+        uint32_t keep0 = rem0 >= 4 ? 0xffffffffu : (rem0 <= 0 ? 0u : ~(0xffffffffu >> (8*rem0)));
+        uint32_t keep1 = rem1 >= 4 ? 0xffffffffu : (rem1 <= 0 ? 0u : ~(0xffffffffu >> (8*rem1)));
+        uint32_t pad0  = (rem0 >= 0 && rem0 < 4) ? (0x80000000u >> (8*rem0)) : 0u;
+        uint32_t pad1  = (rem1 >= 0 && rem1 < 4) ? (0x80000000u >> (8*rem1)) : 0u;
+        hi = (hi & keep0) | pad0;
+        lo = (lo & keep1) | pad1;
+        if( b == nblk-1u && j == 15 ) { hi = total >> 29; lo = total << 3; }
+        if( b == nblk-1u && j == 14 ) { hi = 0u; lo = 0u; }
+      }
+      W[j] = ((uint64_t)hi << 32) | lo;
+    }
+    sha512_compress( h, W );
+  }
+  uint32_t dg[ 16 ];
+#pragma unroll
+  for( int i=0; i<8; i++ ) { dg[2*i] = sha_bswap32( (uint32_t)(h[i] >> 32) ); dg[2*i+1] = sha_bswap32( (uint32_t)h[i] ); }
+  sc_reduce512( k, dg );
+}
+
+__device__ __forceinline__ void atab_store( uint32_t * atab, uint64_t stride, uint64_t gid, int e, ge_cached const & c ) {
+  uint32_t * p = atab + (uint64_t)e * FD_ATAB_WORDS * stride + gid;
+#pragma unroll
+  for( int j=0; j<10; j++ ) {
+    p[ (uint64_t)( 0+j)*stride ] = c.YpX.v[j];
+    p[ (uint64_t)(10+j)*stride ] = c.YmX.v[j];
+    p[ (uint64_t)(20+j)*stride ] = c.T2d.v[j];
+    p[ (uint64_t)(30+j)*stride ] = c.Z2.v[j];
+  }
+}
+
+/* Table entry |d| (biased digit db = d + 8), negated when d < 0. */
+__device__ __forceinline__ void atab_load( ge_cached & c, uint32_t const * atab, uint64_t stride, uint64_t gid, uint32_t db ) {
+  bool neg = db < 8u;
+  uint32_t e = neg ? 8u - db : db - 8u;
+  uint32_t const * p = atab + (uint64_t)e * FD_ATAB_WORDS * stride + gid;
+  fe a, b, t;
+#pragma unroll
+  for( int j=0; j<10; j++ ) {
+    a.v[j]    = p[ (uint64_t)( 0+j)*stride ];
+    b.v[j]    = p[ (uint64_t)(10+j)*stride ];
+    t.v[j]    = p[ (uint64_t)(20+j)*stride ];
+    c.Z2.v[j] = p[ (uint64_t)(30+j)*stride ];
+  }
+  fe tn; fe_neg( tn, t );
+#pragma unroll
+  for( int j=0; j<10; j++ ) {
+    c.YpX.v[j] = neg ? b.v[j] : a.v[j];
+    c.YmX.v[j] = neg ? a.v[j] : b.v[j];
+    c.T2d.v[j] = neg ? tn.v[j] : t.v[j];
+  }
+}
+
+__device__ __forceinline__ void btab_load( ge_precomp & q, uint32_t const * lds_btab, uint32_t db ) {
+  bool neg = db < 128u;
+  uint32_t e = neg ? 128u - db : db - 128u;
+  uint4 const * p = (uint4 const *)(lds_btab + e * FD_BTAB_STRIDE);
+  uint32_t w[ 32 ];
+#pragma unroll
+  for( int j=0; j<8; j++ ) { uint4 v = p[j]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
+  fe t, tn;
+#pragma unroll
+  for( int j=0; j<10; j++ ) t.v[j] = w[20+j];
+  fe_neg( tn, t );
+#pragma unroll
+  for( int j=0; j<10; j++ ) {
+    q.YpX.v[j] = neg ? w[10+j] : w[j];
+    q.YmX.v[j] = neg ? w[j]    : w[10+j];
+    q.T2d.v[j] = neg ? tn.v[j] : t.v[j];
+  }
+}
+
+__global__ void __launch_bounds__( FD_VERIFY_BLOCK, FD_VERIFY_WAVES_PER_EU )
+fd_ed25519_verify_kernel( verify_args args ) {
+  __shared__ uint32_t s_btab[ FD_BTAB_N * FD_BTAB_STRIDE ];
+  __shared__ uint8_t  s_dig[ 96 * FD_VERIFY_BLOCK ];   /* [digit][lane]: 64 k-digits, 32 S-digits */
+
+  for( int i=threadIdx.x; i<FD_BTAB_N*FD_BTAB_STRIDE; i+=blockDim.x ) s_btab[i] = args.btab[i];
+  __syncthreads();
+
+  uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( gid >= args.n ) return;
+
+  fd_ed25519_desc_t d = args.desc[ gid ];
+  uint64_t asz = args.arena_sz;
+  if( (uint64_t)d.sig_off + 64u > asz || (uint64_t)d.pub_off + 32u > asz || (uint64_t)d.msg_off + d.msg_sz > asz ) {
+    args.out[ gid ] = (int8_t)FD_ED25519_GPU_CODE_BAD_DESC;
+    return;
+  }
+  uint32_t lim_dw = (uint32_t)((asz + 3u) >> 2) + 1u;   /* last readable dword (arena padded by 8 bytes) */
+
+  uint32_t sig[ 16 ], pub[ 8 ];
+  load_words<16>( sig, args.arena, d.sig_off, lim_dw );
+  load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
+
+  /* Work is ordered to keep few values live (hash first, then A -> table,
+     then R); the reported code follows the reference's check order
+     (fd_ed25519_user.c:157-198): S, decode A, decode R, small-order A,
+     small-order R, then the group equation. */
+  bool bad_s = !sc_lt_l( sig + 8 );                                      /* :157-159 */
+  uint8_t * dig = s_dig + threadIdx.x;
+  if( !bad_s ) {
+    uint32_t k[ 8 ];
+    hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );    /* :203-206 */
+    uint8_t dk[ 64 ], ds[ 32 ];
+    sc_recode_w4( dk, k );
+    sc_recode_w8( ds, sig + 8 );
+#pragma unroll
+    for( int i=0; i<64; i++ ) dig[ i*FD_VERIFY_BLOCK ] = dk[i];
+#pragma unroll
+    for( int i=0; i<32; i++ ) dig[ (64+i)*FD_VERIFY_BLOCK ] = ds[i];
+  }
+  FE_FENCE();
+
+  uint64_t stride = args.atab_stride;
+  bool okA = false, smallA = false;
+  if( !bad_s ) {
+    ge_p3 A;
+    okA = ge_decode( A, pub, !args.ref_codes );                          /* :162 frombytes_2x */
+    smallA = ge_affine_small_order( A );                                 /* :193-195 */
+    FE_FENCE();
+    if( okA && !smallA ) {
+      /* table of [0..8](-A), cached form (:215 neg, :136-144 table) */
+      ge_p3 nA = A;
+      { fe t; fe_neg( t, A.X ); fe_carry( nA.X, t ); fe_neg( t, A.T ); fe_carry( nA.T, t ); }
+      ge_cached c;
+      ge_p3 id; ge_identity( id );
+      ge_to_cached( c, id );  atab_store( args.atab, stride, gid, 0, c );
+      ge_to_cached( c, nA );  atab_store( args.atab, stride, gid, 1, c );
+      ge_precomp nAp;
+      { fe d2; fe_const_d2( d2 ); fe_add_r( nAp.YpX, nA.Y, nA.X ); fe_sub_r( nAp.YmX, nA.Y, nA.X ); fe_mul( nAp.T2d, nA.T, d2 ); }
+      FE_FENCE();
+      ge_p3 P;
+      ge_dbl( P, nA, true ); ge_to_cached( c, P ); atab_store( args.atab, stride, gid, 2, c );
+#pragma unroll 1
+      for( int e=3; e<=8; e++ ) { ge_madd( P, P, nAp, true ); ge_to_cached( c, P ); atab_store( args.atab, stride, gid, e, c ); FE_FENCE(); }
+    }
+  }
+  FE_FENCE();
+
+  bool okR = false, smallR = false;
+  fe xR, yR;
+  if( !bad_s ) {
+    ge_p3 R;
+    okR = ge_decode( R, sig, !args.ref_codes );
+    smallR = ge_affine_small_order( R );                                 /* :196-198 */
+    xR = R.X; yR = R.Y;
+  }
+  FE_FENCE();
+
+  int code;
+  if     ( bad_s  ) code = FD_ED25519_ERR_SIG;
+  else if( !okA   ) code = args.ref_codes ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;   /* :190-192 */
+  else if( !okR   ) code = FD_ED25519_ERR_SIG;
+  else if( smallA ) code = FD_ED25519_ERR_PUBKEY;
+  else if( smallR ) code = FD_ED25519_ERR_SIG;
+  else              code = 0;
+
+  if( code == 0 ) {
+    /* [k](-A) + [S]B  (replaces fd_ed25519_double_scalar_mul_base, fd_curve25519.c:122-166) */
+    ge_p3 acc; ge_identity( acc );
+#pragma unroll 1
+    for( int i=63; i>=0; i-- ) {
+      if( i < 63 ) {
+        ge_dbl( acc, acc, false ); FE_FENCE(); ge_dbl( acc, acc, false ); FE_FENCE();
+        ge_dbl( acc, acc, false ); FE_FENCE(); ge_dbl( acc, acc, true );  FE_FENCE();
+      }
+      ge_cached q;
+      atab_load( q, args.atab, stride, gid, dig[ i*FD_VERIFY_BLOCK ] );
+      bool even = (i & 1) == 0;
+      FE_FENCE();
+      ge_add_cached( acc, acc, q, even );
+      FE_FENCE();
+      if( even ) {
+        ge_precomp bq;
+        btab_load( bq, s_btab, dig[ (64 + (i>>1))*FD_VERIFY_BLOCK ] );
+        FE_FENCE();
+        ge_madd( acc, acc, bq, false );
+        FE_FENCE();
+      }
+    }
+    ge_p3 Rp; Rp.X = xR; Rp.Y = yR;
+    code = ge_eq_z1( acc, Rp ) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;   /* :225-228 */
+  }
+  args.out[ gid ] = (int8_t)code;
+}
+
+/* ------------------------------------------------------------------ host side */
+
+#define FD_MAX_DEV 16
+
+struct fd_dev_state {
+  int          dev;
+  hipStream_t  stream;
+  hipEvent_t   done;
+  uint32_t *   btab;        /* device */
+  uint32_t *   atab;        /* device, FD_ATAB_N*FD_ATAB_WORDS*atab_cap u32 */
+  uint64_t     atab_cap;    /* lanes */
+  uint8_t *    d_arena;  uint64_t arena_cap;
+  fd_ed25519_desc_t * d_desc; uint64_t desc_cap;
+  int8_t *     d_out;
+  int          busy;
+};
+
+struct fd_ed25519_gpu {
+  int          ndev;
+  uint64_t     max_batch;
+  int          ref_codes;
+  fd_dev_state d[ FD_MAX_DEV ];
+  /* pending async batch */
+  int8_t *     pend_out;
+  uint64_t     pend_cnt;
+  int          pend_active;
+};
+
+#define HIPCK( x ) do { hipError_t _e = (x); if( _e != hipSuccess ) { \
+    fprintf( stderr, "fd_ed25519_gpu: %s failed: %s (%s:%d)\n", #x, hipGetErrorString( _e ), __FILE__, __LINE__ ); \
+    return FD_ED25519_GPU_ERR_LAUNCH; } } while( 0 )
+
+static uint64_t align_up( uint64_t x, uint64_t a ) { return (x + a - 1u) / a * a; }
+
+static int dev_reserve( fd_dev_state * s, uint64_t arena_sz, uint64_t cnt ) {
+  HIPCK( hipSetDevice( s->dev ) );
+  uint64_t need_arena = align_up( arena_sz, 4u ) + 16u;
+  if( need_arena > s->arena_cap ) {
+    if( s->d_arena ) HIPCK( hipFree( s->d_arena ) );
+    s->arena_cap = align_up( need_arena * 5u / 4u, 1u << 20 );
+    if( hipMalloc( &s->d_arena, s->arena_cap ) != hipSuccess ) { s->d_arena = NULL; s->arena_cap = 0; return FD_ED25519_GPU_ERR_OOM; }
+  }
+  if( cnt > s->desc_cap ) {
+    if( s->d_desc ) HIPCK( hipFree( s->d_desc ) );
+    if( s->d_out )  HIPCK( hipFree( s->d_out ) );
+    s->desc_cap = align_up( cnt, 4096u );
+    if( hipMalloc( &s->d_desc, s->desc_cap * sizeof(fd_ed25519_desc_t) ) != hipSuccess ||
+        hipMalloc( &s->d_out, s->desc_cap ) != hipSuccess ) { s->desc_cap = 0; return FD_ED25519_GPU_ERR_OOM; }
+  }
+  return FD_ED25519_GPU_OK;
+}
+
+/* Enqueue kernels over [0, cnt) of device-resident descriptors, chunked to
+   the A-table scratch capacity. */
+static int dev_launch( fd_ed25519_gpu_t * ctx, fd_dev_state * s, uint8_t const * d_arena, uint64_t arena_sz,
+                       fd_ed25519_desc_t const * d_desc, uint64_t cnt, int8_t * d_out, hipStream_t st ) {
+  HIPCK( hipSetDevice( s->dev ) );
+  for( uint64_t off=0; off<cnt; off+=s->atab_cap ) {
+    uint64_t m = cnt - off < s->atab_cap ? cnt - off : s->atab_cap;
+    verify_args a;
+    a.arena = d_arena; a.arena_sz = arena_sz; a.desc = d_desc + off; a.n = m; a.out = d_out + off;
+    a.btab = s->btab; a.atab = s->atab; a.atab_stride = s->atab_cap; a.ref_codes = ctx->ref_codes;
+    uint32_t blocks = (uint32_t)((m + FD_VERIFY_BLOCK - 1u) / FD_VERIFY_BLOCK);
+    hipLaunchKernelGGL( fd_ed25519_verify_kernel, dim3( blocks ), dim3( FD_VERIFY_BLOCK ), 0, st, a );
+    HIPCK( hipGetLastError() );
+  }
+  return FD_ED25519_GPU_OK;
+}
+
+extern "C" {
+
+fd_ed25519_gpu_t *
+fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch ) {
+  int cnt = 0;
+  if( hipGetDeviceCount( &cnt ) != hipSuccess || cnt <= 0 ) return NULL;
+  fd_ed25519_gpu_t * ctx = (fd_ed25519_gpu_t *)calloc( 1, sizeof(fd_ed25519_gpu_t) );
+  if( !ctx ) return NULL;
+  if( !max_batch ) max_batch = 1u << 18;
+  ctx->max_batch = max_batch;
+  if( !device_mask ) { int cur = 0; hipGetDevice( &cur ); device_mask = 1ull << cur; }
+  for( int i=0; i<cnt && i<FD_MAX_DEV; i++ ) {
+    if( !((device_mask >> i) & 1u) ) continue;
+    fd_dev_state * s = &ctx->d[ ctx->ndev ];
+    s->dev = i;
+    if( hipSetDevice( i ) != hipSuccess ) goto fail;
+    if( hipStreamCreateWithFlags( &s->stream, hipStreamNonBlocking ) != hipSuccess ) goto fail;
+    if( hipEventCreateWithFlags( &s->done, hipEventDisableTiming ) != hipSuccess ) goto fail;
+    if( hipMalloc( &s->btab, FD_BTAB_N * FD_BTAB_STRIDE * sizeof(uint32_t) ) != hipSuccess ) goto fail;
+    s->atab_cap = align_up( max_batch, FD_VERIFY_BLOCK );
+    if( hipMalloc( &s->atab, (uint64_t)FD_ATAB_N * FD_ATAB_WORDS * s->atab_cap * sizeof(uint32_t) ) != hipSuccess ) goto fail;
+    ctx->ndev++;
+    hipLaunchKernelGGL( fd_ed25519_btab_init, dim3( 1 ), dim3( 256 ), 0, s->stream, s->btab );
+    if( hipStreamSynchronize( s->stream ) != hipSuccess ) goto fail;
+  }
+  if( !ctx->ndev ) goto fail;
+  return ctx;
+fail:
+  fd_ed25519_gpu_delete( ctx );
+  return NULL;
+}
+
+void
+fd_ed25519_gpu_delete( fd_ed25519_gpu_t * ctx ) {
+  if( !ctx ) return;
+  for( int i=0; i<FD_MAX_DEV; i++ ) {
+    fd_dev_state * s = &ctx->d[i];
+    if( !s->stream && !s->btab ) continue;
+    hipSetDevice( s->dev );
+    if( s->stream ) hipStreamSynchronize( s->stream );
+    if( s->btab )    hipFree( s->btab );
+    if( s->atab )    hipFree( s->atab );
+    if( s->d_arena ) hipFree( s->d_arena );
+    if( s->d_desc )  hipFree( s->d_desc );
+    if( s->d_out )   hipFree( s->d_out );
+    if( s->done )    hipEventDestroy( s->done );
+    if( s->stream )  hipStreamDestroy( s->stream );
+  }
+  free( ctx );
+}
+
+int fd_ed25519_gpu_device_cnt( fd_ed25519_gpu_t const * ctx ) { return ctx ? ctx->ndev : 0; }
+
+int
+fd_ed25519_gpu_set_codes( fd_ed25519_gpu_t * ctx, int flavour ) {
+  if( !ctx || (flavour != FD_ED25519_GPU_CODES_AVX512 && flavour != FD_ED25519_GPU_CODES_REF) ) return FD_ED25519_GPU_ERR_ARG;
+  ctx->ref_codes = flavour;
+  return FD_ED25519_GPU_OK;
+}
+
+static int
+check_descs( uint64_t arena_sz, fd_ed25519_desc_t const * desc, uint64_t n ) {
+  for( uint64_t i=0; i<n; i++ ) {
+    fd_ed25519_desc_t const * d = desc + i;
+    if( (uint64_t)d->sig_off + 64u > arena_sz || (uint64_t)d->pub_off + 32u > arena_sz ||
+        (uint64_t)d->msg_off + d->msg_sz > arena_sz ) return FD_ED25519_GPU_ERR_ARG;
+  }
+  return FD_ED25519_GPU_OK;
+}
+
+int
+fd_ed25519_gpu_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                       fd_ed25519_desc_t const * desc, uint64_t desc_cnt, int8_t * out_code ) {
+  if( !ctx ) return FD_ED25519_GPU_ERR_ARG;
+  if( ctx->pend_active ) return FD_ED25519_GPU_ERR_BUSY;
+  if( desc_cnt && (!arena || !desc || !out_code) ) return FD_ED25519_GPU_ERR_ARG;
+  if( arena_sz > 0xffffffffull + 1ull ) return FD_ED25519_GPU_ERR_ARG;
+  int err = check_descs( arena_sz, desc, desc_cnt );
+  if( err ) return err;
+  ctx->pend_out = out_code; ctx->pend_cnt = desc_cnt; ctx->pend_active = 1;
+  for( int i=0; i<ctx->ndev; i++ ) {
+    fd_dev_state * s = &ctx->d[i];
+    uint64_t lo = desc_cnt * (uint64_t)i / (uint64_t)ctx->ndev;
+    uint64_t hi = desc_cnt * (uint64_t)(i+1) / (uint64_t)ctx->ndev;
+    uint64_t m = hi - lo;
+    s->busy = 0;
+    if( !m ) continue;
+    if( (err = dev_reserve( s, arena_sz, m )) ) { ctx->pend_active = 0; return err; }
+    /* Each device gets the whole arena (descriptors index it freely). */
+    HIPCK( hipMemcpyAsync( s->d_arena, arena, arena_sz, hipMemcpyHostToDevice, s->stream ) );
+    HIPCK( hipMemcpyAsync( s->d_desc, desc + lo, m * sizeof(fd_ed25519_desc_t), hipMemcpyHostToDevice, s->stream ) );
+    if( (err = dev_launch( ctx, s, s->d_arena, arena_sz, s->d_desc, m, s->d_out, s->stream )) ) { ctx->pend_active = 0; return err; }
+    HIPCK( hipMemcpyAsync( out_code + lo, s->d_out, m, hipMemcpyDeviceToHost, s->stream ) );
+    HIPCK( hipEventRecord( s->done, s->stream ) );
+    s->busy = 1;
+  }
+  return FD_ED25519_GPU_OK;
+}
+
+int
+fd_ed25519_gpu_poll( fd_ed25519_gpu_t * ctx ) {
+  if( !ctx ) return FD_ED25519_GPU_ERR_ARG;
+  if( !ctx->pend_active ) return FD_ED25519_GPU_OK;
+  for( int i=0; i<ctx->ndev; i++ ) {
+    fd_dev_state * s = &ctx->d[i];
+    if( !s->busy ) continue;
+    hipSetDevice( s->dev );
+    hipError_t e = hipEventQuery( s->done );
+    if( e == hipErrorNotReady ) return FD_ED25519_GPU_PENDING;
+    if( e != hipSuccess ) { ctx->pend_active = 0; return FD_ED25519_GPU_ERR_LAUNCH; }
+    s->busy = 0;
+  }
+  ctx->pend_active = 0;
+  return FD_ED25519_GPU_OK;
+}
+
+int
+fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                             fd_ed25519_desc_t const * desc, uint64_t desc_cnt, int8_t * out_code ) {
+  int err = fd_ed25519_gpu_submit( ctx, arena, arena_sz, desc, desc_cnt, out_code );
+  if( err ) return err;
+  for( int i=0; i<ctx->ndev; i++ ) {
+    fd_dev_state * s = &ctx->d[i];
+    if( !s->busy ) continue;
+    hipSetDevice( s->dev );
+    if( hipEventSynchronize( s->done ) != hipSuccess ) { ctx->pend_active = 0; return FD_ED25519_GPU_ERR_LAUNCH; }
+  }
+  return fd_ed25519_gpu_poll( ctx );
+}
+
+int
+fd_ed25519_verify_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx, uint8_t const * d_arena, uint64_t arena_sz,
+                                 fd_ed25519_desc_t const * d_desc, uint64_t desc_cnt, int8_t * d_out, void * stream ) {
+  if( !ctx || dev_idx < 0 || dev_idx >= ctx->ndev ) return FD_ED25519_GPU_ERR_ARG;
+  if( !desc_cnt ) return FD_ED25519_GPU_OK;
+  if( !d_arena || !d_desc || !d_out ) return FD_ED25519_GPU_ERR_ARG;
+  fd_dev_state * s = &ctx->d[ dev_idx ];
+  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  return dev_launch( ctx, s, d_arena, arena_sz, d_desc, desc_cnt, d_out, st );
+}
+
+int
+fd_ed25519_gpu_verify( fd_ed25519_gpu_t * ctx, uint8_t const * msg, uint64_t msg_sz,
+                       uint8_t const sig[ 64 ], uint8_t const pub[ 32 ], int * out ) {
+  if( !ctx || !out || !sig || !pub || (msg_sz && !msg) || msg_sz > 0xffffu ) return FD_ED25519_GPU_ERR_ARG;
+  uint64_t sz = 96u + msg_sz;
+  uint8_t * arena = (uint8_t *)malloc( sz + 16u );
+  if( !arena ) return FD_ED25519_GPU_ERR_OOM;
+  memcpy( arena, sig, 64 ); memcpy( arena + 64, pub, 32 ); if( msg_sz ) memcpy( arena + 96, msg, msg_sz );
+  fd_ed25519_desc_t d = { 0u, 64u, 96u, (uint16_t)msg_sz, 0u };
+  int8_t code = 0;
+  int err = fd_ed25519_verify_batch_gpu( ctx, arena, sz, &d, 1u, &code );
+  free( arena );
+  if( err ) return err;
+  *out = code;
+  return FD_ED25519_GPU_OK;
+}
+
+int
+fd_ed25519_gpu_verify_batch_single_msg( fd_ed25519_gpu_t * ctx, uint8_t const * msg, uint64_t msg_sz,
+                                        uint8_t const * sigs, uint8_t const * pubs, uint64_t n, int * out ) {
+  if( !ctx || !out || (msg_sz && !msg) || msg_sz > 0xffffu ) return FD_ED25519_GPU_ERR_ARG;
+  if( n == 0u || n > 16u ) { *out = FD_ED25519_ERR_SIG; return FD_ED25519_GPU_OK; }   /* fd_ed25519_user.c:238-240 */
+  if( !sigs || !pubs ) return FD_ED25519_GPU_ERR_ARG;
+  uint64_t sz = 96u * n + msg_sz;
+  uint8_t * arena = (uint8_t *)malloc( sz + 16u );
+  if( !arena ) return FD_ED25519_GPU_ERR_OOM;
+  memcpy( arena, sigs, 64u * n ); memcpy( arena + 64u * n, pubs, 32u * n );
+  if( msg_sz ) memcpy( arena + 96u * n, msg, msg_sz );
+  fd_ed25519_desc_t d[ 16 ];
+  for( uint64_t j=0; j<n; j++ ) {
+    d[j].sig_off = (uint32_t)(64u * j); d[j].pub_off = (uint32_t)(64u * n + 32u * j);
+    d[j].msg_off = (uint32_t)(96u * n); d[j].msg_sz = (uint16_t)msg_sz; d[j].txn_idx = 0u;
+  }
+  int8_t codes[ 16 ];
+  int err = fd_ed25519_verify_batch_gpu( ctx, arena, sz, d, n, codes );
+  free( arena );
+  if( err ) return err;
+  int8_t t;
+  fd_ed25519_gpu_txn_reduce( codes, d, n, &t, 1u );
+  *out = t;
+  return FD_ED25519_GPU_OK;
+}
+
+int64_t
+fd_ed25519_gpu_txn_reduce( int8_t const * out_code, fd_ed25519_desc_t const * desc, uint64_t n,
+                           int8_t * out_txn_code, uint64_t out_cap ) {
+  int64_t t = 0;
+  uint64_t i = 0;
+  while( i < n ) {
+    uint64_t j = i;
+    while( j < n && desc[j].txn_idx == desc[i].txn_idx ) j++;
+    int8_t code = FD_ED25519_SUCCESS;
+    if( j - i > 16u ) code = FD_ED25519_ERR_SIG;
+    else {
+      int8_t first_p1 = 0, any_msg = 0;
+      for( uint64_t k=i; k<j; k++ ) {
+        int8_t c = out_code[k];
+        if( c == FD_ED25519_ERR_MSG ) any_msg = 1;
+        else if( c != FD_ED25519_SUCCESS && !first_p1 ) first_p1 = c;
+      }
+      code = first_p1 ? first_p1 : (any_msg ? (int8_t)FD_ED25519_ERR_MSG : (int8_t)FD_ED25519_SUCCESS);
+    }
+    if( (uint64_t)t < out_cap ) out_txn_code[t] = code;
+    t++;
+    i = j;
+  }
+  return t;
+}
+
+char const *
+fd_ed25519_gpu_strerror( int err ) {
+  switch( err ) {
+  case FD_ED25519_SUCCESS:         return "success";
+  case FD_ED25519_ERR_SIG:         return "bad signature";
+  case FD_ED25519_ERR_PUBKEY:      return "bad public key";
+  case FD_ED25519_ERR_MSG:         return "bad message";
+  case FD_ED25519_GPU_PENDING:     return "pending";
+  case FD_ED25519_GPU_ERR_NODEV:   return "no gpu device";
+  case FD_ED25519_GPU_ERR_OOM:     return "gpu out of memory";
+  case FD_ED25519_GPU_ERR_LAUNCH:  return "gpu launch/runtime failure";
+  case FD_ED25519_GPU_ERR_ARG:     return "bad argument";
+  case FD_ED25519_GPU_ERR_BUSY:    return "batch already in flight";
+  case FD_ED25519_GPU_CODE_BAD_DESC: return "descriptor outside arena";
+  default: break;
+  }
+  return "unknown";
+}
+
+} /* extern "C" */

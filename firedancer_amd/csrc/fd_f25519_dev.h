@@ -1,0 +1,295 @@
+/* fd_f25519_dev.h -- GF(2^255-19) arithmetic for gfx950, one field element
+   per lane in ten 32-bit VGPRs (radix 2^25.5: limb i sits at bit
+   ceil(25.5*i); even limbs hold 26 bits, odd limbs 25).
+
+   Replaces fd_f25519_* (src/ballet/ed25519/fd_f25519.h:46-253; ref backend
+   5x51 fiat-crypto ref/fd_f25519.h, AVX-512 backend 6x43 r43x6
+   avx512/fd_f25519.h).  Design (measured on MI355X, tools/valu_probe.hip,
+   profiles/r01_valu_probe.json):
+
+   * v_mad_u64_u32 issues at the same rate as every other "half-rate"
+     gfx950 VALU op (mul/mad/add3/alignbit/add_co/addc), ~4.4 cyc per wave
+     instruction per SIMD at 8 waves/SIMD, while add/and/xor/lshr_b32 run at
+     ~2.5.  A saturated 2^32-radix schoolbook needs an add-with-carry per
+     MAC (64 mad + 64 addc per mul); radix 2^25.5 keeps every column sum
+     below 2^64, so each MAC is ONE v_mad_u64_u32 and the column carry is
+     folded into the next column's chain as its initial addend.
+   * Per product: 100 mad (mul) / 55 mad (sqr), +19/x2 premultiplies, one
+     64-bit shift + one AND per column.
+
+   Limb bounds (checked by tests/test_field_bounds.py on the exact limb
+   operations):
+     "R"  (reduced)    even <= 2^26 + 2^11,     odd <= 2^25 + 2^16
+     "M"  (mul input)  even <= 3*2^26 + 2^13, odd <= 3*2^25 + 2^18
+   so any sum of up to three R values, and R + 2p - R, are valid M inputs.
+   fe_mul / fe_sq accept M inputs and return R; fe_add of two R is M;
+   fe_sub(R, R) is M; fe_carry(any limbs < 2^31) is R. */
+
+#ifndef FD_F25519_DEV_H
+#define FD_F25519_DEV_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define FD_FN __device__ __forceinline__
+#else
+#define FD_FN static inline
+#endif
+
+struct fe { uint32_t v[ 10 ]; };
+
+#define FE_M26 0x3ffffffu
+#define FE_M25 0x1ffffffu
+
+/* 2p and 4p in limb form (limb 0 of p is 2^26-19, others 2^26-1 / 2^25-1) */
+#define FE_2P0  (2u*(0x3ffffffu-18u))
+#define FE_2PE  (2u*0x3ffffffu)
+#define FE_2PO  (2u*0x1ffffffu)
+
+/* One 32x32->64 multiply-accumulate.  On the device this is a single
+   v_mad_u64_u32 written as inline asm so the compiler cannot reassociate the
+   column chain into parallel partial sums (which costs an extra 64-bit add
+   per column and ~30 VGPRs per product; measured: a dependent
+   v_mad_u64_u32 chain issues at the same rate as independent ones). */
+#if defined(__HIP_DEVICE_COMPILE__)
+FD_FN uint64_t mad64( uint32_t a, uint32_t b, uint64_t c ) {
+  uint64_t r;
+  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) : "vcc" );
+  return r;
+}
+#else
+FD_FN uint64_t mad64( uint32_t a, uint32_t b, uint64_t c ) { return (uint64_t)a * (uint64_t)b + c; }
+#endif
+
+/* Scheduling fence: keeps the machine scheduler from interleaving
+   independent field products (which raises VGPR pressure past the
+   occupancy target and spills). */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define FE_FENCE() __builtin_amdgcn_sched_barrier( 0 )
+#else
+#define FE_FENCE() do {} while( 0 )
+#endif
+
+FD_FN void fe_set0( fe & r ) { for( int i=0; i<10; i++ ) r.v[i] = 0u; }
+FD_FN void fe_set1( fe & r ) { r.v[0] = 1u; for( int i=1; i<10; i++ ) r.v[i] = 0u; }
+
+FD_FN void fe_add( fe & r, fe const & a, fe const & b ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = a.v[i] + b.v[i];
+}
+
+/* r = a + 2p - b.  Requires b limbs <= 2p limbs (b in R). */
+FD_FN void fe_sub( fe & r, fe const & a, fe const & b ) {
+  r.v[0] = (a.v[0] + FE_2P0) - b.v[0];
+#pragma unroll
+  for( int i=1; i<10; i++ ) r.v[i] = (a.v[i] + ((i&1) ? FE_2PO : FE_2PE)) - b.v[i];
+}
+
+/* One parallel carry round: limbs < 2^31 in, R out. */
+FD_FN void fe_carry( fe & r, fe const & a ) {
+  uint32_t c[ 10 ];
+#pragma unroll
+  for( int i=0; i<10; i++ ) c[i] = a.v[i] >> ((i&1) ? 25 : 26);
+  r.v[0] = (a.v[0] & FE_M26) + 19u*c[9];
+#pragma unroll
+  for( int i=1; i<10; i++ ) r.v[i] = (a.v[i] & ((i&1) ? FE_M25 : FE_M26)) + c[i-1];
+}
+
+FD_FN void fe_add_r( fe & r, fe const & a, fe const & b ) { fe t; fe_add( t, a, b ); fe_carry( r, t ); }
+FD_FN void fe_sub_r( fe & r, fe const & a, fe const & b ) { fe t; fe_sub( t, a, b ); fe_carry( r, t ); }
+
+/* 2p - a (a in R) -> M */
+FD_FN void fe_neg( fe & r, fe const & a ) {
+  r.v[0] = FE_2P0 - a.v[0];
+#pragma unroll
+  for( int i=1; i<10; i++ ) r.v[i] = ((i&1) ? FE_2PO : FE_2PE) - a.v[i];
+}
+
+/* Column finish: split the 64-bit column into its limb and carry the rest
+   into the next column's accumulator. */
+#define FE_COL_DONE( acc, out, sh, msk ) do { (out) = (uint32_t)(acc) & (msk); (acc) = (acc) >> (sh); } while( 0 )
+
+/* h = f*g.  Inputs in M, output in R. */
+FD_FN void fe_mul( fe & h, fe const & f, fe const & g ) {
+  uint32_t f0=f.v[0],f1=f.v[1],f2=f.v[2],f3=f.v[3],f4=f.v[4],f5=f.v[5],f6=f.v[6],f7=f.v[7],f8=f.v[8],f9=f.v[9];
+  uint32_t g0=g.v[0],g1=g.v[1],g2=g.v[2],g3=g.v[3],g4=g.v[4],g5=g.v[5],g6=g.v[6],g7=g.v[7],g8=g.v[8],g9=g.v[9];
+  uint32_t g1_19=19u*g1, g2_19=19u*g2, g3_19=19u*g3, g4_19=19u*g4, g5_19=19u*g5;
+  uint32_t g6_19=19u*g6, g7_19=19u*g7, g8_19=19u*g8, g9_19=19u*g9;
+  uint32_t f1_2=2u*f1, f3_2=2u*f3, f5_2=2u*f5, f7_2=2u*f7, f9_2=2u*f9;
+  uint64_t a;
+  uint32_t h0,h1,h2,h3,h4,h5,h6,h7,h8,h9;
+  a = (uint64_t)f0*g0;
+  a = mad64(f1_2,g9_19,a); a = mad64(f2,g8_19,a); a = mad64(f3_2,g7_19,a); a = mad64(f4,g6_19,a);
+  a = mad64(f5_2,g5_19,a); a = mad64(f6,g4_19,a); a = mad64(f7_2,g3_19,a); a = mad64(f8,g2_19,a); a = mad64(f9_2,g1_19,a);
+  FE_COL_DONE( a, h0, 26, FE_M26 );
+  a = mad64(f0,g1,a); a = mad64(f1,g0,a);
+  a = mad64(f2,g9_19,a); a = mad64(f3,g8_19,a); a = mad64(f4,g7_19,a); a = mad64(f5,g6_19,a);
+  a = mad64(f6,g5_19,a); a = mad64(f7,g4_19,a); a = mad64(f8,g3_19,a); a = mad64(f9,g2_19,a);
+  FE_COL_DONE( a, h1, 25, FE_M25 );
+  a = mad64(f0,g2,a); a = mad64(f1_2,g1,a); a = mad64(f2,g0,a);
+  a = mad64(f3_2,g9_19,a); a = mad64(f4,g8_19,a); a = mad64(f5_2,g7_19,a); a = mad64(f6,g6_19,a);
+  a = mad64(f7_2,g5_19,a); a = mad64(f8,g4_19,a); a = mad64(f9_2,g3_19,a);
+  FE_COL_DONE( a, h2, 26, FE_M26 );
+  a = mad64(f0,g3,a); a = mad64(f1,g2,a); a = mad64(f2,g1,a); a = mad64(f3,g0,a);
+  a = mad64(f4,g9_19,a); a = mad64(f5,g8_19,a); a = mad64(f6,g7_19,a); a = mad64(f7,g6_19,a);
+  a = mad64(f8,g5_19,a); a = mad64(f9,g4_19,a);
+  FE_COL_DONE( a, h3, 25, FE_M25 );
+  a = mad64(f0,g4,a); a = mad64(f1_2,g3,a); a = mad64(f2,g2,a); a = mad64(f3_2,g1,a); a = mad64(f4,g0,a);
+  a = mad64(f5_2,g9_19,a); a = mad64(f6,g8_19,a); a = mad64(f7_2,g7_19,a); a = mad64(f8,g6_19,a); a = mad64(f9_2,g5_19,a);
+  FE_COL_DONE( a, h4, 26, FE_M26 );
+  a = mad64(f0,g5,a); a = mad64(f1,g4,a); a = mad64(f2,g3,a); a = mad64(f3,g2,a); a = mad64(f4,g1,a); a = mad64(f5,g0,a);
+  a = mad64(f6,g9_19,a); a = mad64(f7,g8_19,a); a = mad64(f8,g7_19,a); a = mad64(f9,g6_19,a);
+  FE_COL_DONE( a, h5, 25, FE_M25 );
+  a = mad64(f0,g6,a); a = mad64(f1_2,g5,a); a = mad64(f2,g4,a); a = mad64(f3_2,g3,a); a = mad64(f4,g2,a);
+  a = mad64(f5_2,g1,a); a = mad64(f6,g0,a);
+  a = mad64(f7_2,g9_19,a); a = mad64(f8,g8_19,a); a = mad64(f9_2,g7_19,a);
+  FE_COL_DONE( a, h6, 26, FE_M26 );
+  a = mad64(f0,g7,a); a = mad64(f1,g6,a); a = mad64(f2,g5,a); a = mad64(f3,g4,a); a = mad64(f4,g3,a);
+  a = mad64(f5,g2,a); a = mad64(f6,g1,a); a = mad64(f7,g0,a);
+  a = mad64(f8,g9_19,a); a = mad64(f9,g8_19,a);
+  FE_COL_DONE( a, h7, 25, FE_M25 );
+  a = mad64(f0,g8,a); a = mad64(f1_2,g7,a); a = mad64(f2,g6,a); a = mad64(f3_2,g5,a); a = mad64(f4,g4,a);
+  a = mad64(f5_2,g3,a); a = mad64(f6,g2,a); a = mad64(f7_2,g1,a); a = mad64(f8,g0,a);
+  a = mad64(f9_2,g9_19,a);
+  FE_COL_DONE( a, h8, 26, FE_M26 );
+  a = mad64(f0,g9,a); a = mad64(f1,g8,a); a = mad64(f2,g7,a); a = mad64(f3,g6,a); a = mad64(f4,g5,a);
+  a = mad64(f5,g4,a); a = mad64(f6,g3,a); a = mad64(f7,g2,a); a = mad64(f8,g1,a); a = mad64(f9,g0,a);
+  FE_COL_DONE( a, h9, 25, FE_M25 );
+  /* a = carry out of limb 9 (< 2^37): times 19 back into limb 0 */
+  a = mad64( (uint32_t)a, 19u, (uint64_t)h0 ) + ((uint64_t)(19u*(uint32_t)(a>>32))<<32);
+  h0 = (uint32_t)a & FE_M26;
+  h1 += (uint32_t)(a >> 26);
+  h.v[0]=h0; h.v[1]=h1; h.v[2]=h2; h.v[3]=h3; h.v[4]=h4; h.v[5]=h5; h.v[6]=h6; h.v[7]=h7; h.v[8]=h8; h.v[9]=h9;
+}
+
+/* h = f^2.  Input in M, output in R. */
+FD_FN void fe_sq( fe & h, fe const & f ) {
+  uint32_t f0=f.v[0],f1=f.v[1],f2=f.v[2],f3=f.v[3],f4=f.v[4],f5=f.v[5],f6=f.v[6],f7=f.v[7],f8=f.v[8],f9=f.v[9];
+  uint32_t f0_2=2u*f0, f1_2=2u*f1, f2_2=2u*f2, f3_2=2u*f3, f4_2=2u*f4, f5_2=2u*f5, f6_2=2u*f6, f7_2=2u*f7;
+  uint32_t f5_38=38u*f5, f6_19=19u*f6, f7_38=38u*f7, f8_19=19u*f8, f9_38=38u*f9;
+  uint64_t a;
+  uint32_t h0,h1,h2,h3,h4,h5,h6,h7,h8,h9;
+  a = (uint64_t)f0*f0;
+  a = mad64(f1_2,f9_38,a); a = mad64(f2_2,f8_19,a); a = mad64(f3_2,f7_38,a); a = mad64(f4_2,f6_19,a); a = mad64(f5,f5_38,a);
+  FE_COL_DONE( a, h0, 26, FE_M26 );
+  a = mad64(f0_2,f1,a);
+  a = mad64(f2,f9_38,a); a = mad64(f3_2,f8_19,a); a = mad64(f4,f7_38,a); a = mad64(f5_2,f6_19,a);
+  FE_COL_DONE( a, h1, 25, FE_M25 );
+  a = mad64(f0_2,f2,a); a = mad64(f1_2,f1,a);
+  a = mad64(f3_2,f9_38,a); a = mad64(f4_2,f8_19,a); a = mad64(f5_2,f7_38,a); a = mad64(f6,f6_19,a);
+  FE_COL_DONE( a, h2, 26, FE_M26 );
+  a = mad64(f0_2,f3,a); a = mad64(f1_2,f2,a);
+  a = mad64(f4,f9_38,a); a = mad64(f5_2,f8_19,a); a = mad64(f6,f7_38,a);
+  FE_COL_DONE( a, h3, 25, FE_M25 );
+  a = mad64(f0_2,f4,a); a = mad64(f1_2,f3_2,a); a = mad64(f2,f2,a);
+  a = mad64(f5_2,f9_38,a); a = mad64(f6_2,f8_19,a); a = mad64(f7,f7_38,a);
+  FE_COL_DONE( a, h4, 26, FE_M26 );
+  a = mad64(f0_2,f5,a); a = mad64(f1_2,f4,a); a = mad64(f2_2,f3,a);
+  a = mad64(f6,f9_38,a); a = mad64(f7_2,f8_19,a);
+  FE_COL_DONE( a, h5, 25, FE_M25 );
+  a = mad64(f0_2,f6,a); a = mad64(f1_2,f5_2,a); a = mad64(f2_2,f4,a); a = mad64(f3_2,f3,a);
+  a = mad64(f7_2,f9_38,a); a = mad64(f8,f8_19,a);
+  FE_COL_DONE( a, h6, 26, FE_M26 );
+  a = mad64(f0_2,f7,a); a = mad64(f1_2,f6,a); a = mad64(f2_2,f5,a); a = mad64(f3_2,f4,a);
+  a = mad64(f8,f9_38,a);
+  FE_COL_DONE( a, h7, 25, FE_M25 );
+  a = mad64(f0_2,f8,a); a = mad64(f1_2,f7_2,a); a = mad64(f2_2,f6,a); a = mad64(f3_2,f5_2,a); a = mad64(f4,f4,a);
+  a = mad64(f9,f9_38,a);
+  FE_COL_DONE( a, h8, 26, FE_M26 );
+  a = mad64(f0_2,f9,a); a = mad64(f1_2,f8,a); a = mad64(f2_2,f7,a); a = mad64(f3_2,f6,a); a = mad64(f4_2,f5,a);
+  FE_COL_DONE( a, h9, 25, FE_M25 );
+  a = mad64( (uint32_t)a, 19u, (uint64_t)h0 ) + ((uint64_t)(19u*(uint32_t)(a>>32))<<32);
+  h0 = (uint32_t)a & FE_M26;
+  h1 += (uint32_t)(a >> 26);
+  h.v[0]=h0; h.v[1]=h1; h.v[2]=h2; h.v[3]=h3; h.v[4]=h4; h.v[5]=h5; h.v[6]=h6; h.v[7]=h7; h.v[8]=h8; h.v[9]=h9;
+}
+
+FD_FN void fe_sqn( fe & h, fe const & f, int n ) {
+  fe_sq( h, f );
+#pragma unroll 1
+  for( int i=1; i<n; i++ ) fe_sq( h, h );
+}
+
+/* 2 * f in one multiply-free pass (M in R out not guaranteed: use only on R inputs; result M) */
+FD_FN void fe_dbl( fe & r, fe const & a ) { fe_add( r, a, a ); }
+
+/* Canonical 8x32 little-endian words of f (fully reduced mod p). */
+FD_FN void fe_tobytes32( uint32_t o[ 8 ], fe const & f ) {
+  /* full carry chain to get limbs in range with the value < 2^255 + small */
+  uint32_t h[ 10 ];
+  for( int i=0; i<10; i++ ) h[i] = f.v[i];
+  uint32_t c;
+  for( int pass=0; pass<2; pass++ ) {
+    for( int i=0; i<9; i++ ) { int s = (i&1) ? 25 : 26; c = h[i] >> s; h[i] &= (1u<<s)-1u; h[i+1] += c; }
+    c = h[9] >> 25; h[9] &= FE_M25; h[0] += 19u*c;
+  }
+  /* now h < 2^255 + 2^26 roughly: compute q = (h + 19) >> 255 to subtract p once */
+  uint32_t q = (h[0] + 19u) >> 26;
+  for( int i=1; i<10; i++ ) q = (h[i] + q) >> ((i&1) ? 25 : 26);
+  h[0] += 19u*q;
+  for( int i=0; i<9; i++ ) { int s = (i&1) ? 25 : 26; c = h[i] >> s; h[i] &= (1u<<s)-1u; h[i+1] += c; }
+  h[9] &= FE_M25;
+  /* pack limbs at bit positions 0,26,51,77,102,128,153,179,204,230 */
+  o[0] = h[0]        | (h[1] << 26);
+  o[1] = (h[1] >> 6) | (h[2] << 19);
+  o[2] = (h[2] >> 13)| (h[3] << 13);
+  o[3] = (h[3] >> 19)| (h[4] << 6);
+  o[4] = h[5]        | (h[6] << 25);
+  o[5] = (h[6] >> 7) | (h[7] << 19);
+  o[6] = (h[7] >> 13)| (h[8] << 12);
+  o[7] = (h[8] >> 20)| (h[9] << 6);
+}
+
+/* f from 8 little-endian words, bit 255 ignored (NOT reduced mod p: values
+   in [p, 2^255) are kept as-is, matching fd_f25519_frombytes). */
+FD_FN void fe_frombytes32( fe & f, uint32_t const w[ 8 ] ) {
+  f.v[0] =  w[0]                          & FE_M26;
+  f.v[1] = ((w[0] >> 26) | (w[1] << 6))   & FE_M25;
+  f.v[2] = ((w[1] >> 19) | (w[2] << 13))  & FE_M26;
+  f.v[3] = ((w[2] >> 13) | (w[3] << 19))  & FE_M25;
+  f.v[4] =  (w[3] >> 6)                   & FE_M26;
+  f.v[5] =  w[4]                          & FE_M25;
+  f.v[6] = ((w[4] >> 25) | (w[5] << 7))   & FE_M26;
+  f.v[7] = ((w[5] >> 19) | (w[6] << 13))  & FE_M25;
+  f.v[8] = ((w[6] >> 12) | (w[7] << 20))  & FE_M26;
+  f.v[9] =  (w[7] >> 6)                   & FE_M25;
+}
+
+FD_FN int fe_is_zero( fe const & f ) {
+  uint32_t o[ 8 ]; fe_tobytes32( o, f );
+  return !(o[0]|o[1]|o[2]|o[3]|o[4]|o[5]|o[6]|o[7]);
+}
+
+/* parity of the canonical value (fd_f25519_sgn) */
+FD_FN int fe_sgn( fe const & f ) { uint32_t o[ 8 ]; fe_tobytes32( o, f ); return (int)(o[0] & 1u); }
+
+FD_FN int fe_eq( fe const & a, fe const & b ) { fe d; fe_sub( d, a, b ); fe_carry( d, d ); return fe_is_zero( d ); }
+
+/* a^(2^252-3) (replaces fd_f25519_pow22523, src/ballet/ed25519/fd_f25519.c:10-59) */
+FD_FN void fe_pow22523( fe & out, fe const & z ) {
+  fe t0, t1, t2;
+  fe_sq( t0, z );                 /* 2 */
+  fe_sqn( t1, t0, 2 );            /* 8 */
+  fe_mul( t1, z, t1 );            /* 9 */
+  fe_mul( t0, t0, t1 );           /* 11 */
+  fe_sq( t0, t0 );                /* 22 */
+  fe_mul( t0, t1, t0 );           /* 31 = 2^5-1 */
+  fe_sqn( t1, t0, 5 );
+  fe_mul( t0, t1, t0 );           /* 2^10-1 */
+  fe_sqn( t1, t0, 10 );
+  fe_mul( t1, t1, t0 );           /* 2^20-1 */
+  fe_sqn( t2, t1, 20 );
+  fe_mul( t1, t2, t1 );           /* 2^40-1 */
+  fe_sqn( t1, t1, 10 );
+  fe_mul( t0, t1, t0 );           /* 2^50-1 */
+  fe_sqn( t1, t0, 50 );
+  fe_mul( t1, t1, t0 );           /* 2^100-1 */
+  fe_sqn( t2, t1, 100 );
+  fe_mul( t1, t2, t1 );           /* 2^200-1 */
+  fe_sqn( t1, t1, 50 );
+  fe_mul( t0, t1, t0 );           /* 2^250-1 */
+  fe_sqn( t0, t0, 2 );            /* 2^252-4 */
+  fe_mul( out, t0, z );           /* 2^252-3 */
+}
+
+#endif /* FD_F25519_DEV_H */

@@ -1,0 +1,129 @@
+/* fd_scalar_dev.h -- scalars mod l on 32-bit words, per lane.
+
+   l = 2^252 + 27742317777372353535851937790883648493.
+   Replaces fd_curve25519_scalar_validate (src/ballet/ed25519/
+   fd_curve25519_scalar.h:57-73) and fd_curve25519_scalar_reduce
+   (fd_curve25519_scalar.c:3-110).  The reference's wNAF recoding
+   (fd_curve25519_scalar_wnaf, :277-360) is replaced by fixed-width signed
+   windows (fd_scalar_recode_*), which keeps every lane of a wave on the
+   same add schedule (no divergence), at the cost of a few more additions. */
+
+#ifndef FD_SCALAR_DEV_H
+#define FD_SCALAR_DEV_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define FD_SC_FN __device__ __forceinline__
+#else
+#define FD_SC_FN static inline
+#endif
+
+/* l as 8 LE words */
+#define FD_L0 0x5cf5d3edu
+#define FD_L1 0x5812631au
+#define FD_L2 0xa2f79cd6u
+#define FD_L3 0x14def9deu
+#define FD_L7 0x10000000u
+
+/* s <= l-1, i.e. s < l, as a 256-bit LE integer: the S check of
+   fd_ed25519_verify (fd_ed25519_user.c:157-159).  Bits 253..255 of s are
+   NOT masked (s >= 2^253 is rejected). */
+FD_SC_FN int sc_lt_l( uint32_t const s[ 8 ] ) {
+  uint32_t const l[ 8 ] = { FD_L0, FD_L1, FD_L2, FD_L3, 0u, 0u, 0u, FD_L7 };
+  int lt = 0, eq = 1;
+#pragma unroll
+  for( int i=7; i>=0; i-- ) {
+    lt |= eq & (s[i] < l[i]);
+    eq &= (s[i] == l[i]);
+  }
+  return lt;
+}
+
+/* r = x mod l for a 512-bit x (16 LE words).  Barrett with b = 2^32, k = 8,
+   mu = floor(2^512 / l) (derived constant, 9 words). */
+FD_SC_FN void sc_reduce512( uint32_t r[ 8 ], uint32_t const x[ 16 ] ) {
+  uint32_t const mu[ 9 ] = { 0x0a2c131bu, 0xed9ce5a3u, 0x086329a7u, 0x2106215du, 0xffffffebu,
+                             0xffffffffu, 0xffffffffu, 0xffffffffu, 0x0000000fu };
+  uint32_t const l[ 8 ] = { FD_L0, FD_L1, FD_L2, FD_L3, 0u, 0u, 0u, FD_L7 };
+  /* q1 = floor(x / b^7): words 7..15 (9 words); q2 = q1*mu; q3 = floor(q2 / b^9) */
+  uint32_t q2[ 18 ];
+#pragma unroll
+  for( int i=0; i<18; i++ ) q2[i] = 0u;
+#pragma unroll
+  for( int i=0; i<9; i++ ) {
+    uint64_t c = 0;
+#pragma unroll
+    for( int j=0; j<9; j++ ) {
+      uint64_t t = (uint64_t)x[7+i] * mu[j] + q2[i+j] + c;
+      q2[i+j] = (uint32_t)t; c = t >> 32;
+    }
+    q2[i+9] = (uint32_t)c;
+  }
+  /* r2 = (q3 * l) mod b^9, q3 = q2[9..17] */
+  uint32_t r2[ 9 ];
+#pragma unroll
+  for( int i=0; i<9; i++ ) r2[i] = 0u;
+#pragma unroll
+  for( int i=0; i<9; i++ ) {
+    uint64_t c = 0;
+#pragma unroll
+    for( int j=0; j<8; j++ ) {
+      if( i+j<9 ) {
+        uint64_t t = (uint64_t)q2[9+i] * l[j] + r2[i+j] + c;
+        r2[i+j] = (uint32_t)t; c = t >> 32;
+      }
+    }
+    if( i+8<9 ) r2[i+8] = (uint32_t)c;
+  }
+  /* r = (x mod b^9) - r2 mod b^9, then at most two subtractions of l */
+  uint32_t t9[ 9 ];
+  uint64_t br = 0;
+#pragma unroll
+  for( int i=0; i<9; i++ ) {
+    uint64_t d = (uint64_t)x[i] - r2[i] - br;
+    t9[i] = (uint32_t)d; br = (d >> 63) & 1u;
+  }
+#pragma unroll
+  for( int it=0; it<2; it++ ) {
+    /* t9 >= l ? subtract */
+    uint32_t s9[ 9 ]; uint64_t b2 = 0;
+#pragma unroll
+    for( int i=0; i<9; i++ ) {
+      uint64_t d = (uint64_t)t9[i] - (i<8 ? l[i] : 0u) - b2;
+      s9[i] = (uint32_t)d; b2 = (d >> 63) & 1u;
+    }
+    int ge = (b2 == 0);
+#pragma unroll
+    for( int i=0; i<9; i++ ) t9[i] = ge ? s9[i] : t9[i];
+  }
+#pragma unroll
+  for( int i=0; i<8; i++ ) r[i] = t9[i];
+}
+
+/* Signed fixed-window recoding.  s (< 2^253) = sum_i d_i 2^(w i) with
+   d_i in [-2^(w-1), 2^(w-1)-1] for all but possibly the top digit.  The
+   digits are emitted as (d + 2^(w-1)) biased bytes so they fit a u8. */
+FD_SC_FN void sc_recode_w4( uint8_t out[ 64 ], uint32_t const s[ 8 ] ) {
+  int c = 0;
+#pragma unroll
+  for( int i=0; i<64; i++ ) {
+    int d = (int)((s[i>>3] >> (4*(i&7))) & 15u) + c;
+    c = d >= 8;
+    d -= c << 4;
+    out[i] = (uint8_t)(d + 8);
+  }
+}
+
+FD_SC_FN void sc_recode_w8( uint8_t out[ 32 ], uint32_t const s[ 8 ] ) {
+  int c = 0;
+#pragma unroll
+  for( int i=0; i<32; i++ ) {
+    int d = (int)((s[i>>2] >> (8*(i&3))) & 255u) + c;
+    c = d >= 128;
+    d -= c << 8;
+    out[i] = (uint8_t)(d + 128);
+  }
+}
+
+#endif /* FD_SCALAR_DEV_H */

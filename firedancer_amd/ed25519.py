@@ -1,0 +1,184 @@
+"""ctypes mirror of include/fd_ed25519_gpu.h (see package docstring)."""
+import ctypes
+import os
+
+import numpy as np
+
+FD_ED25519_SUCCESS = 0
+FD_ED25519_ERR_SIG = -1
+FD_ED25519_ERR_PUBKEY = -2
+FD_ED25519_ERR_MSG = -3
+CODE_BAD_DESC = -128
+
+GPU_OK = 0
+GPU_PENDING = 1
+
+CODES_AVX512 = 0
+CODES_REF = 1
+
+# fd_ed25519_desc_t (16 bytes, include/fd_ed25519_gpu.h)
+DESC_DTYPE = np.dtype([("sig_off", "<u4"), ("pub_off", "<u4"), ("msg_off", "<u4"),
+                       ("msg_sz", "<u2"), ("txn_idx", "<u2")])
+assert DESC_DTYPE.itemsize == 16
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class GpuError(RuntimeError):
+    pass
+
+
+def lib_path():
+    return os.path.join(_HERE, "libfd_ed25519_gpu.so")
+
+
+def load_lib():
+    """Load the in-tree HIP library (raises if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    try:  # share torch's HIP runtime if torch is used in this process (same SONAME, one runtime)
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(path):
+        raise GpuError("libfd_ed25519_gpu.so not built (run `make -C firedancer_amd` or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    lib.fd_ed25519_gpu_new.restype = vp
+    lib.fd_ed25519_gpu_new.argtypes = [u64, u64]
+    lib.fd_ed25519_gpu_delete.argtypes = [vp]
+    lib.fd_ed25519_gpu_device_cnt.argtypes = [vp]
+    lib.fd_ed25519_gpu_set_codes.argtypes = [vp, i32]
+    lib.fd_ed25519_verify_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
+    lib.fd_ed25519_gpu_submit.argtypes = [vp, vp, u64, vp, u64, vp]
+    lib.fd_ed25519_gpu_poll.argtypes = [vp]
+    lib.fd_ed25519_verify_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_verify.argtypes = [vp, ctypes.c_char_p, u64, ctypes.c_char_p, ctypes.c_char_p,
+                                          ctypes.POINTER(ctypes.c_int)]
+    lib.fd_ed25519_gpu_verify_batch_single_msg.argtypes = [vp, ctypes.c_char_p, u64, ctypes.c_char_p,
+                                                           ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int)]
+    lib.fd_ed25519_gpu_txn_reduce.restype = ctypes.c_int64
+    lib.fd_ed25519_gpu_txn_reduce.argtypes = [vp, vp, u64, vp, u64]
+    lib.fd_ed25519_gpu_strerror.restype = ctypes.c_char_p
+    lib.fd_ed25519_gpu_strerror.argtypes = [i32]
+    _LIB = lib
+    return lib
+
+
+def strerror(code):
+    return load_lib().fd_ed25519_gpu_strerror(int(code)).decode()
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def pack_batch(records):
+    """records: iterable of (msg, sig, pub[, txn_idx]) bytes -> (arena uint8 array, desc array).
+
+    Layout: sig | pub | msg per record, packed back to back with no alignment
+    (the kernel reads unaligned fields), like payload bytes in a dcache chunk."""
+    recs = list(records)
+    n = len(recs)
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    total = sum(96 + len(r[0]) for r in recs)
+    arena = np.zeros(total + 16, dtype=np.uint8)
+    off = 0
+    for i, r in enumerate(recs):
+        msg, sig, pub = r[0], r[1], r[2]
+        txn = r[3] if len(r) > 3 else i & 0xffff
+        arena[off:off + 64] = np.frombuffer(sig, np.uint8)
+        arena[off + 64:off + 96] = np.frombuffer(pub, np.uint8)
+        if msg:
+            arena[off + 96:off + 96 + len(msg)] = np.frombuffer(msg, np.uint8)
+        desc[i] = (off, off + 64, off + 96, len(msg), txn)
+        off += 96 + len(msg)
+    return arena, desc, total
+
+
+def txn_reduce(codes, desc):
+    """Per-txn codes with the fd_ed25519_verify_batch_single_msg precedence (host function, no GPU)."""
+    lib = load_lib()
+    codes = np.ascontiguousarray(codes, dtype=np.int8)
+    desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    out = np.zeros(max(len(desc), 1), dtype=np.int8)
+    t = lib.fd_ed25519_gpu_txn_reduce(_ptr(codes), _ptr(desc), len(desc), _ptr(out), len(out))
+    return out[:t].copy()
+
+
+class Ed25519Gpu:
+    """One verify context (fd_ed25519_gpu_t) over the GPUs in device_mask."""
+
+    def __init__(self, device_mask=0, max_batch=1 << 18, codes=CODES_AVX512):
+        self.lib = load_lib()
+        self.ctx = self.lib.fd_ed25519_gpu_new(device_mask, max_batch)
+        if not self.ctx:
+            raise GpuError("fd_ed25519_gpu_new failed (no HIP device?)")
+        self.set_codes(codes)
+
+    def close(self):
+        if self.ctx:
+            self.lib.fd_ed25519_gpu_delete(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def device_cnt(self):
+        return self.lib.fd_ed25519_gpu_device_cnt(self.ctx)
+
+    def set_codes(self, flavour):
+        r = self.lib.fd_ed25519_gpu_set_codes(self.ctx, flavour)
+        if r:
+            raise GpuError(strerror(r))
+
+    def verify_batch(self, arena, arena_sz, desc):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        out = np.zeros(len(desc), dtype=np.int8)
+        r = self.lib.fd_ed25519_verify_batch_gpu(self.ctx, _ptr(arena), arena_sz, _ptr(desc), len(desc), _ptr(out))
+        if r:
+            raise GpuError("fd_ed25519_verify_batch_gpu: %s (%d)" % (strerror(r), r))
+        return out
+
+    def submit(self, arena, arena_sz, desc, out):
+        self._keep = (arena, desc, out)
+        r = self.lib.fd_ed25519_gpu_submit(self.ctx, _ptr(arena), arena_sz, _ptr(desc), len(desc), _ptr(out))
+        if r:
+            raise GpuError("fd_ed25519_gpu_submit: %s (%d)" % (strerror(r), r))
+
+    def poll(self):
+        r = self.lib.fd_ed25519_gpu_poll(self.ctx)
+        if r < 0:
+            raise GpuError("fd_ed25519_gpu_poll: %s (%d)" % (strerror(r), r))
+        return r == GPU_OK
+
+    def verify_batch_dev(self, d_arena, arena_sz, d_desc, desc_cnt, d_out, stream=0, dev_idx=0):
+        """Device pointers (ints), enqueue only."""
+        r = self.lib.fd_ed25519_verify_batch_gpu_dev(self.ctx, dev_idx, d_arena, arena_sz, d_desc, desc_cnt,
+                                                     d_out, stream)
+        if r:
+            raise GpuError("fd_ed25519_verify_batch_gpu_dev: %s (%d)" % (strerror(r), r))
+
+    def verify(self, msg, sig, pub):
+        """Mirror of fd_ed25519_verify: returns the FD_ED25519_* code."""
+        out = ctypes.c_int(0)
+        r = self.lib.fd_ed25519_gpu_verify(self.ctx, msg, len(msg), sig, pub, ctypes.byref(out))
+        if r:
+            raise GpuError(strerror(r))
+        return out.value
+
+    def verify_batch_single_msg(self, msg, sigs, pubs, n):
+        """Mirror of fd_ed25519_verify_batch_single_msg (sigs/pubs concatenated bytes)."""
+        out = ctypes.c_int(0)
+        r = self.lib.fd_ed25519_gpu_verify_batch_single_msg(self.ctx, msg, len(msg), sigs or b"\0" * 64,
+                                                            pubs or b"\0" * 32, n, ctypes.byref(out))
+        if r:
+            raise GpuError(strerror(r))
+        return out.value

@@ -1,0 +1,137 @@
+/* fd_ed25519_gpu.h -- C ABI of the MI355X Ed25519 batch verifier.
+
+   Drop-in boundary for the reference verify path.  Plain
+   C types only; link against firedancer_amd/libfd_ed25519_gpu.so.
+
+   Reference interfaces replaced:
+     fd_ed25519_verify                   src/ballet/ed25519/fd_ed25519.h:96-101
+                                         (impl src/ballet/ed25519/fd_ed25519_user.c:134-229)
+     fd_ed25519_verify_batch_single_msg  src/ballet/ed25519/fd_ed25519.h:120-126
+                                         (impl fd_ed25519_user.c:231-309)
+     fd_ed25519_strerror                 src/ballet/ed25519/fd_ed25519.h:134-135
+     the per-txn call of fd_txn_verify   src/app/fdctl/run/tiles/fd_verify.h:43-88 (line 74)
+
+   Result codes per signature are bit-exact with the reference
+   fd_ed25519_verify built with FD_HAS_AVX512 (FD_ED25519_SUCCESS / _ERR_SIG
+   / _ERR_PUBKEY / _ERR_MSG, src/ballet/ed25519/fd_ed25519.h:11-14).  The
+   return value of every call is reserved for infrastructure status
+   (FD_ED25519_GPU_OK or FD_ED25519_GPU_ERR_*, all <= -100), so it can never
+   be confused with a verify code. */
+
+#ifndef FD_ED25519_GPU_H
+#define FD_ED25519_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Verify codes (same values as src/ballet/ed25519/fd_ed25519.h:11-14) */
+#define FD_ED25519_SUCCESS     ( 0)
+#define FD_ED25519_ERR_SIG     (-1)
+#define FD_ED25519_ERR_PUBKEY  (-2)
+#define FD_ED25519_ERR_MSG     (-3)
+
+/* Per-signature out_code for a descriptor pointing outside the arena (only
+   produced by the device-pointer entry point; the host entry points reject
+   such batches with FD_ED25519_GPU_ERR_ARG before launching). */
+#define FD_ED25519_GPU_CODE_BAD_DESC (-128)
+
+/* Infrastructure status (return values) */
+#define FD_ED25519_GPU_OK          (0)
+#define FD_ED25519_GPU_PENDING     (1)
+#define FD_ED25519_GPU_ERR_NODEV   (-100)
+#define FD_ED25519_GPU_ERR_OOM     (-101)
+#define FD_ED25519_GPU_ERR_LAUNCH  (-102)
+#define FD_ED25519_GPU_ERR_ARG     (-103)
+#define FD_ED25519_GPU_ERR_BUSY    (-104)
+
+/* Which reference build's error codes to reproduce (they differ only in how
+   a public key that fails to decode is reported: SURVEY.md §8(a) A4/A5). */
+#define FD_ED25519_GPU_CODES_AVX512 (0)   /* default: FD_HAS_AVX512 build */
+#define FD_ED25519_GPU_CODES_REF    (1)   /* portable ref build           */
+
+/* One signature to verify.  Offsets are bytes from the arena base (e.g. the
+   dcache chunk0 address, so a registered workspace can be addressed
+   directly).  msg may be empty (msg_sz 0).  txn_idx groups signatures of
+   one transaction for fd_ed25519_gpu_txn_reduce (descriptors of one txn
+   must be contiguous and in signature order). */
+typedef struct {
+  uint32_t sig_off;   /* 64 bytes: R || S   */
+  uint32_t pub_off;   /* 32 bytes: A        */
+  uint32_t msg_off;
+  uint16_t msg_sz;    /* <= 65535 (txn MTU is 1232) */
+  uint16_t txn_idx;
+} fd_ed25519_desc_t;
+
+typedef struct fd_ed25519_gpu fd_ed25519_gpu_t;
+
+/* Create a context over the GPUs in device_mask (bit i = HIP device i;
+   0 = the calling thread's current device).  max_batch bounds the number of
+   descriptors per call (device buffers are sized for it; larger calls are
+   split internally).  Returns NULL on failure (no device / OOM). */
+fd_ed25519_gpu_t * fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch );
+void               fd_ed25519_gpu_delete( fd_ed25519_gpu_t * ctx );
+int                fd_ed25519_gpu_device_cnt( fd_ed25519_gpu_t const * ctx );
+
+/* Select the error-code flavour (FD_ED25519_GPU_CODES_*). */
+int fd_ed25519_gpu_set_codes( fd_ed25519_gpu_t * ctx, int flavour );
+
+/* Synchronous batch verify over host memory: arena[0, arena_sz) and desc are
+   copied to the GPU(s), the batch is sharded contiguously over the context's
+   devices, and out_code[i] receives the code of desc[i].  Read interest in
+   arena/desc and write interest in out_code for the duration of the call. */
+int fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t *        ctx,
+                                 uint8_t const *           arena,
+                                 uint64_t                  arena_sz,
+                                 fd_ed25519_desc_t const * desc,
+                                 uint64_t                  desc_cnt,
+                                 int8_t *                  out_code );
+
+/* Asynchronous pair (wiredancer-style push model, src/wiredancer/c/wd_f1.h:71-112):
+   submit enqueues the copies + kernels and returns; poll returns
+   FD_ED25519_GPU_PENDING until every device finished, then FD_ED25519_GPU_OK
+   (out_code valid) or an error.  One batch in flight per context.  The caller
+   keeps arena/desc/out_code alive until poll reports completion. */
+int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                           fd_ed25519_desc_t const * desc, uint64_t desc_cnt, int8_t * out_code );
+int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * ctx );
+
+/* Device-resident entry point (no host copies): d_arena / d_desc / d_out are
+   device pointers on the context's device dev_idx, stream is a hipStream_t
+   (NULL = the context's own stream for that device).  d_arena must be
+   readable up to align_up(arena_sz, 4) + 8 bytes.  Enqueues and returns. */
+int fd_ed25519_verify_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx,
+                                     uint8_t const * d_arena, uint64_t arena_sz,
+                                     fd_ed25519_desc_t const * d_desc, uint64_t desc_cnt,
+                                     int8_t * d_out, void * stream );
+
+/* Single-signature and single-message-batch drop-ins (host memory, synchronous).
+   *out receives the verify code exactly as fd_ed25519_verify /
+   fd_ed25519_verify_batch_single_msg would return it (batch: n==0 or n>16 ->
+   FD_ED25519_ERR_SIG, phase-1 errors in index order first, then ERR_MSG). */
+int fd_ed25519_gpu_verify( fd_ed25519_gpu_t * ctx, uint8_t const * msg, uint64_t msg_sz,
+                           uint8_t const sig[ 64 ], uint8_t const pub[ 32 ], int * out );
+int fd_ed25519_gpu_verify_batch_single_msg( fd_ed25519_gpu_t * ctx, uint8_t const * msg, uint64_t msg_sz,
+                                            uint8_t const * sigs, uint8_t const * pubs, uint64_t n, int * out );
+
+/* Host helper: fold per-signature codes into per-transaction codes with the
+   two-phase precedence of fd_ed25519_verify_batch_single_msg
+   (fd_ed25519_user.c:231-309): the first (lowest index) ERR_SIG/ERR_PUBKEY
+   of a txn wins, else ERR_MSG if any signature failed the equation, else
+   SUCCESS.  A txn's signatures are the maximal runs of equal txn_idx.
+   out_txn_code[t] is written for the t-th run; returns the run count, or
+   FD_ED25519_GPU_ERR_ARG if a run is longer than 16 (reported as
+   FD_ED25519_ERR_SIG for that run, like the reference's batch_sz>16). */
+int64_t fd_ed25519_gpu_txn_reduce( int8_t const * out_code, fd_ed25519_desc_t const * desc, uint64_t n,
+                                   int8_t * out_txn_code, uint64_t out_cap );
+
+char const * fd_ed25519_gpu_strerror( int err );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FD_ED25519_GPU_H */

@@ -1,0 +1,22 @@
+// field_host_check.cpp -- TEST ONLY: compiles the device field header for the
+// host so tests/test_field_bounds.py can drive fe_mul/fe_sq/... with limb
+// vectors at the documented bounds and compare against Python big ints.
+#include "../../firedancer_amd/csrc/fd_f25519_dev.h"
+extern "C" {
+void t_mul( uint32_t * h, uint32_t const * f, uint32_t const * g ) { fe a, b, r; for( int i=0;i<10;i++ ){a.v[i]=f[i];b.v[i]=g[i];} fe_mul( r, a, b ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_sq ( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_sq( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_sub( uint32_t * h, uint32_t const * f, uint32_t const * g ) { fe a, b, r; for( int i=0;i<10;i++ ){a.v[i]=f[i];b.v[i]=g[i];} fe_sub( r, a, b ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_carry( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_carry( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_tobytes( uint32_t * o, uint32_t const * f ) { fe a; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_tobytes32( o, a ); }
+void t_frombytes( uint32_t * h, uint32_t const * w ) { fe a; fe_frombytes32( a, w ); for( int i=0;i<10;i++ ) h[i]=a.v[i]; }
+void t_pow22523( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_pow22523( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+}
+#include "../../firedancer_amd/csrc/fd_scalar_dev.h"
+#include "../../firedancer_amd/csrc/fd_sha512_dev.h"
+extern "C" {
+void t_sc_reduce( uint32_t * r, uint32_t const * x ) { sc_reduce512( r, x ); }
+int  t_sc_lt_l( uint32_t const * s ) { return sc_lt_l( s ); }
+void t_recode4( uint8_t * o, uint32_t const * s ) { sc_recode_w4( o, s ); }
+void t_recode8( uint8_t * o, uint32_t const * s ) { sc_recode_w8( o, s ); }
+void t_sha_block( uint64_t * h, uint64_t * w ) { sha512_compress( h, w ); }
+}

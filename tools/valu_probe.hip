@@ -17,8 +17,11 @@
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return 1; } } while (0)
 
-constexpr int ILP   = 12;
-constexpr int ITERS = 2048;
+#ifndef PROBE_ILP
+#define PROBE_ILP 12
+#endif
+constexpr int ILP   = PROBE_ILP;
+constexpr int ITERS = 16384 / ILP * 12 / 4;
 
 // clk[0] = sum over waves of s_memtime delta, clk[1] = sum of s_memrealtime delta
 #define PROLOGUE \
@@ -72,6 +75,13 @@ K32(k_perm_b32,        "v_perm_b32 %0, %1, %0, %2")
 K32(k_xor_b32,         "v_xor_b32 %0, %1, %0")
 K32(k_bfi_b32,         "v_bfi_b32 %0, %1, %2, %0")
 K32(k_lshl_add_u32,    "v_lshl_add_u32 %0, %1, 3, %0")
+K32(k_add_u32_e64,     "v_add_u32_e64 %0, %1, %0")
+K32(k_mul_u32_u24,     "v_mul_u32_u24 %0, %1, %0")
+K32(k_and_b32,         "v_and_b32 %0, %1, %0")
+K32(k_lshrrev_b32,     "v_lshrrev_b32 %0, %1, %0")
+K32(k_xor_b32_e64,     "v_xor_b32_e64 %0, %1, %0")
+K32(k_add_co_vcc_pair, "v_add_co_u32_e32 %0, vcc, %1, %0\n\tv_addc_co_u32_e32 %0, vcc, %2, %0, vcc")
+K32(k_cndmask_vcc,     "v_cndmask_b32_e32 %0, %1, %0, vcc")
 
 // add with carry chain: v_add_co_u32 then v_addc_co_u32 through vcc-like SGPR pair
 __global__ void k_add_co_addc(uint32_t* out, uint64_t* clk, uint32_t seed) {
@@ -172,6 +182,9 @@ int main(int argc, char** argv) {
     {"v_lshl_add_u32", k_lshl_add_u32, 1}, {"v_add_co+v_addc_co(pair)", k_add_co_addc, 2},
     {"v_fma_f64", k_fma_f64, 1}, {"v_fma_f32", k_fma_f32, 1}, {"v_lshrrev_b64", k_lshrrev_b64, 1},
     {"v_mad_u64_u32+v_addc(pair)", k_mad_addc_pair, 2},
+    {"v_add_u32_e64", k_add_u32_e64, 1}, {"v_mul_u32_u24", k_mul_u32_u24, 1}, {"v_and_b32", k_and_b32, 1},
+    {"v_lshrrev_b32", k_lshrrev_b32, 1}, {"v_xor_b32_e64", k_xor_b32_e64, 1},
+    {"v_add_co_e32+v_addc_e32(vcc pair)", k_add_co_vcc_pair, 2}, {"v_cndmask_b32_e32", k_cndmask_vcc, 1},
   };
   hipDeviceProp_t prop; CHECK(hipGetDeviceProperties(&prop, 0));
   int cus = prop.multiProcessorCount;
@@ -182,7 +195,7 @@ int main(int argc, char** argv) {
   printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d, \"ilp\": %d, \"iters\": %d, \"probes\": [\n",
          prop.gcnArchName, cus, prop.clockRate, ILP, ITERS);
   int first = 1;
-  int wps_list[] = {1, 2, 4};
+  int wps_list[] = {2, 4, 8};
   for (auto& p : probes) {
     for (int wps : wps_list) {
       int threads = 256;                       // 4 waves per workgroup
