@@ -1,0 +1,125 @@
+"""CPU: the device arithmetic headers (firedancer_amd/csrc/*_dev.h) compiled for
+the host and driven at the documented limb bounds against Python big ints.
+This pins the radix-2^25.5 bound bookkeeping (R / M bounds, no 64-bit column
+overflow) and the scalar / SHA helpers the kernel uses."""
+import ctypes
+import hashlib
+import os
+import random
+import struct
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = 2**255 - 19
+LL = 2**252 + 27742317777372353535851937790883648493
+POS = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+R_E, R_O = 2**26 + 2**11, 2**25 + 2**16
+M_E, M_O = 3 * 2**26 + 2**13, 3 * 2**25 + 2**18
+
+
+@pytest.fixture(scope="module")
+def lib():
+    out = os.path.join(REPO, "tests", "_build")
+    os.makedirs(out, exist_ok=True)
+    so = os.path.join(out, "field_host_check.so")
+    src = os.path.join(REPO, "tests", "csrc", "field_host_check.cpp")
+    subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-o", so, src])
+    return ctypes.CDLL(so)
+
+
+def val(l):
+    return sum(x << POS[i] for i, x in enumerate(l))
+
+
+def arr(l, t=ctypes.c_uint32):
+    return (t * len(l))(*l)
+
+
+def limbs_at(be, bo, mode, rng):
+    return [(be if i % 2 == 0 else bo) if mode == "max" else rng.randrange(0, (be if i % 2 == 0 else bo) + 1)
+            for i in range(10)]
+
+
+def in_R(h):
+    return all(x <= (R_E if i % 2 == 0 else R_O) for i, x in enumerate(h))
+
+
+def test_mul_sq_at_bounds(lib):
+    rng = random.Random(1)
+    for it in range(3000):
+        mode = "max" if it < 20 else "rand"
+        f = limbs_at(M_E, M_O, mode, rng); g = limbs_at(M_E, M_O, mode, rng)
+        h = (ctypes.c_uint32 * 10)(); lib.t_mul(h, arr(f), arr(g)); h = list(h)
+        assert val(h) % P == val(f) * val(g) % P and in_R(h)
+        h = (ctypes.c_uint32 * 10)(); lib.t_sq(h, arr(f)); h = list(h)
+        assert val(h) % P == val(f) ** 2 % P and in_R(h)
+
+
+def test_sub_carry_canon(lib):
+    rng = random.Random(2)
+    for it in range(3000):
+        mode = "max" if it < 20 else "rand"
+        a = limbs_at(R_E, R_O, mode, rng); b = limbs_at(R_E, R_O, mode, rng)
+        h = (ctypes.c_uint32 * 10)(); lib.t_sub(h, arr(a), arr(b)); h = list(h)
+        assert val(h) % P == (val(a) - val(b)) % P
+        assert all(x <= (M_E if i % 2 == 0 else M_O) for i, x in enumerate(h))
+        c = [rng.randrange(0, 2**31) for _ in range(10)] if mode == "rand" else [2**31 - 1] * 10
+        h = (ctypes.c_uint32 * 10)(); lib.t_carry(h, arr(c)); h = list(h)
+        assert val(h) % P == val(c) % P and in_R(h)
+        f = limbs_at(M_E, M_O, mode, rng)
+        o = (ctypes.c_uint32 * 8)(); lib.t_tobytes(o, arr(f))
+        assert sum(x << (32 * i) for i, x in enumerate(o)) == val(f) % P
+    for v in [0, 1, P - 1, P, P + 1, P + 18, 2**255 - 1]:
+        lim = [(v >> POS[i]) & ((1 << (26 if i % 2 == 0 else 25)) - 1) for i in range(10)]
+        o = (ctypes.c_uint32 * 8)(); lib.t_tobytes(o, arr(lim))
+        assert sum(x << (32 * i) for i, x in enumerate(o)) == v % P
+
+
+def test_frombytes_not_reduced(lib):
+    rng = random.Random(3)
+    for _ in range(500):
+        w = [rng.randrange(0, 2**32) for _ in range(8)]
+        h = (ctypes.c_uint32 * 10)(); lib.t_frombytes(h, arr(w))
+        assert val(list(h)) == sum(x << (32 * i) for i, x in enumerate(w)) % 2**255   # bit 255 dropped only
+
+
+def test_pow22523(lib):
+    rng = random.Random(4)
+    for _ in range(20):
+        f = limbs_at(R_E, R_O, "rand", rng)
+        h = (ctypes.c_uint32 * 10)(); lib.t_pow22523(h, arr(f))
+        assert val(list(h)) % P == pow(val(f), 2**252 - 3, P)
+
+
+def test_scalar_reduce_and_check(lib):
+    rng = random.Random(5)
+    edge = [0, 1, LL, LL - 1, LL + 1, 2**512 - 1, LL * 3, 2**252, 2**511, LL * 2**259]
+    for it in range(20000):
+        x = edge[it] if it < len(edge) else rng.getrandbits(512)
+        r = (ctypes.c_uint32 * 8)(); lib.t_sc_reduce(r, arr([(x >> (32 * i)) & 0xffffffff for i in range(16)]))
+        assert sum(v << (32 * i) for i, v in enumerate(r)) == x % LL
+    lib.t_sc_lt_l.restype = ctypes.c_int
+    for s in [LL - 1, LL, LL + 1, 0, 2**256 - 1, 2**253, LL - 2**200, 2**252]:
+        assert lib.t_sc_lt_l(arr([(s >> (32 * i)) & 0xffffffff for i in range(8)])) == (s < LL)
+
+
+def test_recoding(lib):
+    rng = random.Random(6)
+    for it in range(3000):
+        s = rng.getrandbits(253) if it else LL - 1
+        w = arr([(s >> (32 * i)) & 0xffffffff for i in range(8)])
+        o4 = (ctypes.c_uint8 * 64)(); lib.t_recode4(o4, w)
+        assert sum((d - 8) * 16**i for i, d in enumerate(o4)) == s and all(0 <= d <= 16 for d in o4)
+        o8 = (ctypes.c_uint8 * 32)(); lib.t_recode8(o8, w)
+        assert sum((d - 128) * 256**i for i, d in enumerate(o8)) == s
+
+
+def test_sha512_block(lib):
+    iv = [0x6a09e667f3bcc908, 0xbb67ae8584caa73b, 0x3c6ef372fe94f82b, 0xa54ff53a5f1d36f1,
+          0x510e527fade682d1, 0x9b05688c2b3e6c1f, 0x1f83d9abfb41bd6b, 0x5be0cd19137e2179]
+    h = arr(iv, ctypes.c_uint64)
+    w = arr([0x8000000000000000] + [0] * 15, ctypes.c_uint64)
+    lib.t_sha_block(h, w)
+    assert b"".join(struct.pack(">Q", v) for v in h) == hashlib.sha512(b"").digest()
