@@ -147,36 +147,50 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
   sc_reduce512( k, dg );
 }
 
-__device__ __forceinline__ void atab_store( uint32_t * atab, uint64_t stride, uint64_t gid, int e, ge_cached const & c ) {
-  uint32_t * p = atab + (uint64_t)e * FD_ATAB_WORDS * stride + gid;
+/* A-table layout: entry e of lane g = 40 words (Y+X, Y-X, 2dT, 2Z; 10 limbs
+   each) split into a 128-byte record main[e][g][32] (one cache line, read with
+   8 x 16-B loads) and a 32-byte record tail[e][g][8] (4 lanes per line), so a
+   lane's entry is fetched with no over-read whatever entry its digit selects. */
+__device__ __forceinline__ void atab_ptrs( uint32_t const * atab, uint64_t cap, uint64_t gid, uint32_t e,
+                                           uint4 const ** m, uint4 const ** t ) {
+  uint64_t idx = (uint64_t)e * cap + gid;
+  *m = (uint4 const *)(atab + idx * 32u);
+  *t = (uint4 const *)(atab + (uint64_t)FD_ATAB_N * cap * 32u + idx * 8u);
+}
+
+__device__ __forceinline__ void atab_store( uint32_t * atab, uint64_t cap, uint64_t gid, int e, ge_cached const & c ) {
+  uint32_t w[ 40 ];
 #pragma unroll
-  for( int j=0; j<10; j++ ) {
-    p[ (uint64_t)( 0+j)*stride ] = c.YpX.v[j];
-    p[ (uint64_t)(10+j)*stride ] = c.YmX.v[j];
-    p[ (uint64_t)(20+j)*stride ] = c.T2d.v[j];
-    p[ (uint64_t)(30+j)*stride ] = c.Z2.v[j];
-  }
+  for( int j=0; j<10; j++ ) { w[j] = c.YpX.v[j]; w[10+j] = c.YmX.v[j]; w[20+j] = c.T2d.v[j]; w[30+j] = c.Z2.v[j]; }
+  uint4 const * mc; uint4 const * tc;
+  atab_ptrs( atab, cap, gid, (uint32_t)e, &mc, &tc );
+  uint4 * m = (uint4 *)mc; uint4 * t = (uint4 *)tc;
+#pragma unroll
+  for( int j=0; j<8; j++ ) m[j] = make_uint4( w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
+#pragma unroll
+  for( int j=0; j<2; j++ ) t[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
 }
 
 /* Table entry |d| (biased digit db = d + 8), negated when d < 0. */
-__device__ __forceinline__ void atab_load( ge_cached & c, uint32_t const * atab, uint64_t stride, uint64_t gid, uint32_t db ) {
+__device__ __forceinline__ void atab_load( ge_cached & c, uint32_t const * atab, uint64_t cap, uint64_t gid, uint32_t db ) {
   bool neg = db < 8u;
   uint32_t e = neg ? 8u - db : db - 8u;
-  uint32_t const * p = atab + (uint64_t)e * FD_ATAB_WORDS * stride + gid;
-  fe a, b, t;
+  uint4 const * m; uint4 const * t;
+  atab_ptrs( atab, cap, gid, e, &m, &t );
+  uint32_t w[ 40 ];
+#pragma unroll
+  for( int j=0; j<8; j++ ) { uint4 v = m[j]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
+#pragma unroll
+  for( int j=0; j<2; j++ ) { uint4 v = t[j]; w[32+4*j] = v.x; w[33+4*j] = v.y; w[34+4*j] = v.z; w[35+4*j] = v.w; }
+  fe tv, tn;
+#pragma unroll
+  for( int j=0; j<10; j++ ) { tv.v[j] = w[20+j]; c.Z2.v[j] = w[30+j]; }
+  fe_neg( tn, tv );
 #pragma unroll
   for( int j=0; j<10; j++ ) {
-    a.v[j]    = p[ (uint64_t)( 0+j)*stride ];
-    b.v[j]    = p[ (uint64_t)(10+j)*stride ];
-    t.v[j]    = p[ (uint64_t)(20+j)*stride ];
-    c.Z2.v[j] = p[ (uint64_t)(30+j)*stride ];
-  }
-  fe tn; fe_neg( tn, t );
-#pragma unroll
-  for( int j=0; j<10; j++ ) {
-    c.YpX.v[j] = neg ? b.v[j] : a.v[j];
-    c.YmX.v[j] = neg ? a.v[j] : b.v[j];
-    c.T2d.v[j] = neg ? tn.v[j] : t.v[j];
+    c.YpX.v[j] = neg ? w[10+j] : w[j];
+    c.YmX.v[j] = neg ? w[j]    : w[10+j];
+    c.T2d.v[j] = neg ? tn.v[j] : tv.v[j];
   }
 }
 
@@ -290,10 +304,11 @@ fd_ed25519_verify_kernel( verify_args args ) {
     ge_p3 acc; ge_identity( acc );
 #pragma unroll 1
     for( int i=63; i>=0; i-- ) {
-      if( i < 63 ) {
-        ge_dbl( acc, acc, false ); FE_FENCE(); ge_dbl( acc, acc, false ); FE_FENCE();
-        ge_dbl( acc, acc, false ); FE_FENCE(); ge_dbl( acc, acc, true );  FE_FENCE();
-      }
+      /* 4 doublings as a real loop: the unrolled body (4 x ~3k instructions)
+         overflows the 64 KB instruction cache shared by a CU pair and a lone
+         wave per SIMD then stalls on instruction fetch. */
+#pragma unroll 1
+      for( int j=(i < 63 ? 0 : 4); j<4; j++ ) { ge_dbl( acc, acc, j == 3 ); FE_FENCE(); }
       ge_cached q;
       atab_load( q, args.atab, stride, gid, dig[ i*FD_VERIFY_BLOCK ] );
       bool even = (i & 1) == 0;

@@ -46,19 +46,48 @@ struct fe { uint32_t v[ 10 ]; };
 #define FE_2PE  (2u*0x3ffffffu)
 #define FE_2PO  (2u*0x1ffffffu)
 
-/* One 32x32->64 multiply-accumulate.  On the device this is a single
-   v_mad_u64_u32 written as inline asm so the compiler cannot reassociate the
-   column chain into parallel partial sums (which costs an extra 64-bit add
-   per column and ~30 VGPRs per product; measured: a dependent
-   v_mad_u64_u32 chain issues at the same rate as independent ones). */
+/* 32x32->64 multiply-accumulate chains.  On the device each column of a
+   product is ONE inline-asm block of dependent v_mad_u64_u32 (carry-out to
+   vcc, discarded): the compiler can neither re-associate the chain into
+   parallel partial sums (an extra 64-bit add per column and ~30 VGPRs) nor
+   pad each single-instruction asm statement with an s_nop, which its inline
+   asm hazard check does between back-to-back asm statements.  A dependent
+   v_mad_u64_u32 chain was measured to issue at the rate of independent ones
+   (tools/valu_probe.hip, ILP 1 vs 12). */
 #if defined(__HIP_DEVICE_COMPILE__)
 FD_FN uint64_t mad64( uint32_t a, uint32_t b, uint64_t c ) {
-  uint64_t r;
-  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) : "vcc" );
-  return r;
+  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b) : "vcc" );
+  return c;
+}
+FD_FN uint64_t col5( uint64_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2,
+                     uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4 ) {
+  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %3, %4, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %5, %6, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %7, %8, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %9, %10, %0"
+       : "+v"(c) : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4) : "vcc" );
+  return c;
 }
 #else
 FD_FN uint64_t mad64( uint32_t a, uint32_t b, uint64_t c ) { return (uint64_t)a * (uint64_t)b + c; }
+FD_FN uint64_t col5( uint64_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2,
+                     uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4 ) {
+  return c + (uint64_t)a0*b0 + (uint64_t)a1*b1 + (uint64_t)a2*b2 + (uint64_t)a3*b3 + (uint64_t)a4*b4;
+}
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define COL10( c, a0,b0,a1,b1,a2,b2,a3,b3,a4,b4,a5,b5,a6,b6,a7,b7,a8,b8,a9,b9 ) ({ uint64_t _c = (c); \
+  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %4, %0\n\t"         \
+       "v_mad_u64_u32 %0, vcc, %5, %6, %0\n\tv_mad_u64_u32 %0, vcc, %7, %8, %0\n\t"         \
+       "v_mad_u64_u32 %0, vcc, %9, %10, %0\n\tv_mad_u64_u32 %0, vcc, %11, %12, %0\n\t"      \
+       "v_mad_u64_u32 %0, vcc, %13, %14, %0\n\tv_mad_u64_u32 %0, vcc, %15, %16, %0\n\t"     \
+       "v_mad_u64_u32 %0, vcc, %17, %18, %0\n\tv_mad_u64_u32 %0, vcc, %19, %20, %0"           \
+       : "+v"(_c) : "v"(a0),"v"(b0),"v"(a1),"v"(b1),"v"(a2),"v"(b2),"v"(a3),"v"(b3),"v"(a4),"v"(b4), \
+                    "v"(a5),"v"(b5),"v"(a6),"v"(b6),"v"(a7),"v"(b7),"v"(a8),"v"(b8),"v"(a9),"v"(b9) : "vcc" ); _c; })
+#else
+#define COL10( c, a0,b0,a1,b1,a2,b2,a3,b3,a4,b4,a5,b5,a6,b6,a7,b7,a8,b8,a9,b9 ) \
+  col5( col5( (c), a0,b0,a1,b1,a2,b2,a3,b3,a4,b4 ), a5,b5,a6,b6,a7,b7,a8,b8,a9,b9 )
 #endif
 
 /* Scheduling fence: keeps the machine scheduler from interleaving
@@ -116,44 +145,27 @@ FD_FN void fe_mul( fe & h, fe const & f, fe const & g ) {
   uint32_t g1_19=19u*g1, g2_19=19u*g2, g3_19=19u*g3, g4_19=19u*g4, g5_19=19u*g5;
   uint32_t g6_19=19u*g6, g7_19=19u*g7, g8_19=19u*g8, g9_19=19u*g9;
   uint32_t f1_2=2u*f1, f3_2=2u*f3, f5_2=2u*f5, f7_2=2u*f7, f9_2=2u*f9;
-  uint64_t a;
+  uint64_t a = 0;
   uint32_t h0,h1,h2,h3,h4,h5,h6,h7,h8,h9;
-  a = (uint64_t)f0*g0;
-  a = mad64(f1_2,g9_19,a); a = mad64(f2,g8_19,a); a = mad64(f3_2,g7_19,a); a = mad64(f4,g6_19,a);
-  a = mad64(f5_2,g5_19,a); a = mad64(f6,g4_19,a); a = mad64(f7_2,g3_19,a); a = mad64(f8,g2_19,a); a = mad64(f9_2,g1_19,a);
+  a = COL10( a, f0,g0, f1_2,g9_19, f2,g8_19, f3_2,g7_19, f4,g6_19, f5_2,g5_19, f6,g4_19, f7_2,g3_19, f8,g2_19, f9_2,g1_19 );
   FE_COL_DONE( a, h0, 26, FE_M26 );
-  a = mad64(f0,g1,a); a = mad64(f1,g0,a);
-  a = mad64(f2,g9_19,a); a = mad64(f3,g8_19,a); a = mad64(f4,g7_19,a); a = mad64(f5,g6_19,a);
-  a = mad64(f6,g5_19,a); a = mad64(f7,g4_19,a); a = mad64(f8,g3_19,a); a = mad64(f9,g2_19,a);
+  a = COL10( a, f0,g1, f1,g0, f2,g9_19, f3,g8_19, f4,g7_19, f5,g6_19, f6,g5_19, f7,g4_19, f8,g3_19, f9,g2_19 );
   FE_COL_DONE( a, h1, 25, FE_M25 );
-  a = mad64(f0,g2,a); a = mad64(f1_2,g1,a); a = mad64(f2,g0,a);
-  a = mad64(f3_2,g9_19,a); a = mad64(f4,g8_19,a); a = mad64(f5_2,g7_19,a); a = mad64(f6,g6_19,a);
-  a = mad64(f7_2,g5_19,a); a = mad64(f8,g4_19,a); a = mad64(f9_2,g3_19,a);
+  a = COL10( a, f0,g2, f1_2,g1, f2,g0, f3_2,g9_19, f4,g8_19, f5_2,g7_19, f6,g6_19, f7_2,g5_19, f8,g4_19, f9_2,g3_19 );
   FE_COL_DONE( a, h2, 26, FE_M26 );
-  a = mad64(f0,g3,a); a = mad64(f1,g2,a); a = mad64(f2,g1,a); a = mad64(f3,g0,a);
-  a = mad64(f4,g9_19,a); a = mad64(f5,g8_19,a); a = mad64(f6,g7_19,a); a = mad64(f7,g6_19,a);
-  a = mad64(f8,g5_19,a); a = mad64(f9,g4_19,a);
+  a = COL10( a, f0,g3, f1,g2, f2,g1, f3,g0, f4,g9_19, f5,g8_19, f6,g7_19, f7,g6_19, f8,g5_19, f9,g4_19 );
   FE_COL_DONE( a, h3, 25, FE_M25 );
-  a = mad64(f0,g4,a); a = mad64(f1_2,g3,a); a = mad64(f2,g2,a); a = mad64(f3_2,g1,a); a = mad64(f4,g0,a);
-  a = mad64(f5_2,g9_19,a); a = mad64(f6,g8_19,a); a = mad64(f7_2,g7_19,a); a = mad64(f8,g6_19,a); a = mad64(f9_2,g5_19,a);
+  a = COL10( a, f0,g4, f1_2,g3, f2,g2, f3_2,g1, f4,g0, f5_2,g9_19, f6,g8_19, f7_2,g7_19, f8,g6_19, f9_2,g5_19 );
   FE_COL_DONE( a, h4, 26, FE_M26 );
-  a = mad64(f0,g5,a); a = mad64(f1,g4,a); a = mad64(f2,g3,a); a = mad64(f3,g2,a); a = mad64(f4,g1,a); a = mad64(f5,g0,a);
-  a = mad64(f6,g9_19,a); a = mad64(f7,g8_19,a); a = mad64(f8,g7_19,a); a = mad64(f9,g6_19,a);
+  a = COL10( a, f0,g5, f1,g4, f2,g3, f3,g2, f4,g1, f5,g0, f6,g9_19, f7,g8_19, f8,g7_19, f9,g6_19 );
   FE_COL_DONE( a, h5, 25, FE_M25 );
-  a = mad64(f0,g6,a); a = mad64(f1_2,g5,a); a = mad64(f2,g4,a); a = mad64(f3_2,g3,a); a = mad64(f4,g2,a);
-  a = mad64(f5_2,g1,a); a = mad64(f6,g0,a);
-  a = mad64(f7_2,g9_19,a); a = mad64(f8,g8_19,a); a = mad64(f9_2,g7_19,a);
+  a = COL10( a, f0,g6, f1_2,g5, f2,g4, f3_2,g3, f4,g2, f5_2,g1, f6,g0, f7_2,g9_19, f8,g8_19, f9_2,g7_19 );
   FE_COL_DONE( a, h6, 26, FE_M26 );
-  a = mad64(f0,g7,a); a = mad64(f1,g6,a); a = mad64(f2,g5,a); a = mad64(f3,g4,a); a = mad64(f4,g3,a);
-  a = mad64(f5,g2,a); a = mad64(f6,g1,a); a = mad64(f7,g0,a);
-  a = mad64(f8,g9_19,a); a = mad64(f9,g8_19,a);
+  a = COL10( a, f0,g7, f1,g6, f2,g5, f3,g4, f4,g3, f5,g2, f6,g1, f7,g0, f8,g9_19, f9,g8_19 );
   FE_COL_DONE( a, h7, 25, FE_M25 );
-  a = mad64(f0,g8,a); a = mad64(f1_2,g7,a); a = mad64(f2,g6,a); a = mad64(f3_2,g5,a); a = mad64(f4,g4,a);
-  a = mad64(f5_2,g3,a); a = mad64(f6,g2,a); a = mad64(f7_2,g1,a); a = mad64(f8,g0,a);
-  a = mad64(f9_2,g9_19,a);
+  a = COL10( a, f0,g8, f1_2,g7, f2,g6, f3_2,g5, f4,g4, f5_2,g3, f6,g2, f7_2,g1, f8,g0, f9_2,g9_19 );
   FE_COL_DONE( a, h8, 26, FE_M26 );
-  a = mad64(f0,g9,a); a = mad64(f1,g8,a); a = mad64(f2,g7,a); a = mad64(f3,g6,a); a = mad64(f4,g5,a);
-  a = mad64(f5,g4,a); a = mad64(f6,g3,a); a = mad64(f7,g2,a); a = mad64(f8,g1,a); a = mad64(f9,g0,a);
+  a = COL10( a, f0,g9, f1,g8, f2,g7, f3,g6, f4,g5, f5,g4, f6,g3, f7,g2, f8,g1, f9,g0 );
   FE_COL_DONE( a, h9, 25, FE_M25 );
   /* a = carry out of limb 9 (< 2^37): times 19 back into limb 0 */
   a = mad64( (uint32_t)a, 19u, (uint64_t)h0 ) + ((uint64_t)(19u*(uint32_t)(a>>32))<<32);
@@ -169,34 +181,25 @@ FD_FN void fe_sq( fe & h, fe const & f ) {
   uint32_t f5_38=38u*f5, f6_19=19u*f6, f7_38=38u*f7, f8_19=19u*f8, f9_38=38u*f9;
   uint64_t a;
   uint32_t h0,h1,h2,h3,h4,h5,h6,h7,h8,h9;
-  a = (uint64_t)f0*f0;
-  a = mad64(f1_2,f9_38,a); a = mad64(f2_2,f8_19,a); a = mad64(f3_2,f7_38,a); a = mad64(f4_2,f6_19,a); a = mad64(f5,f5_38,a);
+  a = col5( (uint64_t)f0*f0, f1_2,f9_38, f2_2,f8_19, f3_2,f7_38, f4_2,f6_19, f5,f5_38 );
   FE_COL_DONE( a, h0, 26, FE_M26 );
-  a = mad64(f0_2,f1,a);
-  a = mad64(f2,f9_38,a); a = mad64(f3_2,f8_19,a); a = mad64(f4,f7_38,a); a = mad64(f5_2,f6_19,a);
+  a = col5( a, f0_2,f1, f2,f9_38, f3_2,f8_19, f4,f7_38, f5_2,f6_19 );
   FE_COL_DONE( a, h1, 25, FE_M25 );
-  a = mad64(f0_2,f2,a); a = mad64(f1_2,f1,a);
-  a = mad64(f3_2,f9_38,a); a = mad64(f4_2,f8_19,a); a = mad64(f5_2,f7_38,a); a = mad64(f6,f6_19,a);
+  a = mad64( f0_2,f2, col5( a, f1_2,f1, f3_2,f9_38, f4_2,f8_19, f5_2,f7_38, f6,f6_19 ) );
   FE_COL_DONE( a, h2, 26, FE_M26 );
-  a = mad64(f0_2,f3,a); a = mad64(f1_2,f2,a);
-  a = mad64(f4,f9_38,a); a = mad64(f5_2,f8_19,a); a = mad64(f6,f7_38,a);
+  a = col5( a, f0_2,f3, f1_2,f2, f4,f9_38, f5_2,f8_19, f6,f7_38 );
   FE_COL_DONE( a, h3, 25, FE_M25 );
-  a = mad64(f0_2,f4,a); a = mad64(f1_2,f3_2,a); a = mad64(f2,f2,a);
-  a = mad64(f5_2,f9_38,a); a = mad64(f6_2,f8_19,a); a = mad64(f7,f7_38,a);
+  a = mad64( f0_2,f4, col5( a, f1_2,f3_2, f2,f2, f5_2,f9_38, f6_2,f8_19, f7,f7_38 ) );
   FE_COL_DONE( a, h4, 26, FE_M26 );
-  a = mad64(f0_2,f5,a); a = mad64(f1_2,f4,a); a = mad64(f2_2,f3,a);
-  a = mad64(f6,f9_38,a); a = mad64(f7_2,f8_19,a);
+  a = col5( a, f0_2,f5, f1_2,f4, f2_2,f3, f6,f9_38, f7_2,f8_19 );
   FE_COL_DONE( a, h5, 25, FE_M25 );
-  a = mad64(f0_2,f6,a); a = mad64(f1_2,f5_2,a); a = mad64(f2_2,f4,a); a = mad64(f3_2,f3,a);
-  a = mad64(f7_2,f9_38,a); a = mad64(f8,f8_19,a);
+  a = mad64( f0_2,f6, col5( a, f1_2,f5_2, f2_2,f4, f3_2,f3, f7_2,f9_38, f8,f8_19 ) );
   FE_COL_DONE( a, h6, 26, FE_M26 );
-  a = mad64(f0_2,f7,a); a = mad64(f1_2,f6,a); a = mad64(f2_2,f5,a); a = mad64(f3_2,f4,a);
-  a = mad64(f8,f9_38,a);
+  a = col5( a, f0_2,f7, f1_2,f6, f2_2,f5, f3_2,f4, f8,f9_38 );
   FE_COL_DONE( a, h7, 25, FE_M25 );
-  a = mad64(f0_2,f8,a); a = mad64(f1_2,f7_2,a); a = mad64(f2_2,f6,a); a = mad64(f3_2,f5_2,a); a = mad64(f4,f4,a);
-  a = mad64(f9,f9_38,a);
+  a = mad64( f0_2,f8, col5( a, f1_2,f7_2, f2_2,f6, f3_2,f5_2, f4,f4, f9,f9_38 ) );
   FE_COL_DONE( a, h8, 26, FE_M26 );
-  a = mad64(f0_2,f9,a); a = mad64(f1_2,f8,a); a = mad64(f2_2,f7,a); a = mad64(f3_2,f6,a); a = mad64(f4_2,f5,a);
+  a = col5( a, f0_2,f9, f1_2,f8, f2_2,f7, f3_2,f6, f4_2,f5 );
   FE_COL_DONE( a, h9, 25, FE_M25 );
   a = mad64( (uint32_t)a, 19u, (uint64_t)h0 ) + ((uint64_t)(19u*(uint32_t)(a>>32))<<32);
   h0 = (uint32_t)a & FE_M26;
