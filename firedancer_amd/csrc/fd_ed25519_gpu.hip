@@ -26,15 +26,25 @@
 #include "fd_curve25519_dev.h"
 #include "fd_sha512_dev.h"
 #include "fd_scalar_dev.h"
+#include "fd_lattice_dev.h"
 
-#define FD_VERIFY_BLOCK   256          /* threads per workgroup              */
+#define FD_VERIFY_BLOCK   256          /* threads per workgroup: 4 waves              */
 #ifndef FD_VERIFY_WAVES_PER_EU
-#define FD_VERIFY_WAVES_PER_EU 2       /* -> <= 256 VGPR+AGPR per lane       */
+#define FD_VERIFY_WAVES_PER_EU 2       /* -> <= 256 VGPR+AGPR per lane                */
 #endif
-#define FD_BTAB_N         129          /* [0..128]B                          */
-#define FD_BTAB_STRIDE    32           /* u32 per entry: 3 x 10 limbs + pad  */
-#define FD_ATAB_N         9            /* [0..8](-A)                         */
-#define FD_ATAB_WORDS     40           /* u32 per entry (4 fe)               */
+#define FD_BTAB_N         129          /* [0..128]P                                   */
+#define FD_BTAB_STRIDE    32           /* u32 per entry: 3 x 10 limbs + pad           */
+#define FD_BTAB_WORDS     (2 * FD_BTAB_N * FD_BTAB_STRIDE)   /* P = B and P = 2^128 B */
+#define FD_VTAB_N         9            /* [0..8](-Q), Q = A or R                      */
+#define FD_VTAB_WORDS     40           /* u32 per entry (4 fe)                        */
+#define FD_NDIG_MAX       64           /* 4-bit windows of a <= 256-bit scalar        */
+
+/* LDS digit rows ([row][slot] bytes) */
+#define FD_ROW_U          0            /* signed 4-bit digits of u (sign folded in)   */
+#define FD_ROW_V          64           /* signed 4-bit digits of v                    */
+#define FD_ROW_W          128          /* signed 8-bit digits of w = v S mod l (32)   */
+#define FD_ROW_NW         160          /* lane 0 of each wave: the wave's window count */
+#define FD_ROWS           161
 
 /* ------------------------------------------------------------------ loads */
 
@@ -53,33 +63,42 @@ __device__ __forceinline__ void load_words( uint32_t out[ N ], uint8_t const * a
   }
 }
 
-/* ------------------------------------------------------------------ B table */
+/* ------------------------------------------------------------------ B tables */
 
-/* Device init: lane i computes [i]B and stores its affine precomputed form
-   (Y+X, Y-X, 2dXY) into btab[i*FD_BTAB_STRIDE ...].  B decoded from its
-   standard encoding (y = 4/5, x even). */
+__device__ void ge_affine_precomp( ge_precomp & q, ge_p3 & p ) {
+  fe zi, x, y, xy, d2;
+  fe_invert( zi, p.Z );
+  fe_mul( x, p.X, zi ); fe_mul( y, p.Y, zi );
+  fe_const_d2( d2 );
+  fe_add_r( q.YpX, y, x ); fe_sub_r( q.YmX, y, x ); fe_mul( xy, x, y ); fe_mul( q.T2d, xy, d2 );
+  p.X = x; p.Y = y; fe_set1( p.Z ); p.T = xy;
+}
+
+/* Device init: thread (t, i) computes [i]P_t, P_0 = B, P_1 = 2^128 B, and
+   stores its affine precomputed form (Y+X, Y-X, 2dXY) at
+   btab[(t*FD_BTAB_N + i)*FD_BTAB_STRIDE ...].  B decoded from its standard
+   encoding (y = 4/5, x even). */
 __global__ void fd_ed25519_btab_init( uint32_t * btab ) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if( i >= FD_BTAB_N ) return;
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if( g >= 2*FD_BTAB_N ) return;
+  int t = g / FD_BTAB_N, i = g % FD_BTAB_N;
   uint32_t benc[ 8 ];
   benc[0] = 0x66666658u;
 #pragma unroll
   for( int j=1; j<8; j++ ) benc[j] = 0x66666666u;
   ge_p3 B; ge_decode( B, benc, true );
-  ge_precomp Bp;
-  { fe d2; fe_const_d2( d2 ); fe_add_r( Bp.YpX, B.Y, B.X ); fe_sub_r( Bp.YmX, B.Y, B.X ); fe_mul( Bp.T2d, B.T, d2 ); }
+  if( t ) {
+    for( int j=0; j<128; j++ ) ge_dbl( B, B, true );
+  }
+  ge_precomp Bp; ge_affine_precomp( Bp, B );
   ge_p3 acc; ge_identity( acc );
   for( int bit=7; bit>=0; bit-- ) {
     ge_dbl( acc, acc, true );
     if( (i >> bit) & 1 ) ge_madd( acc, acc, Bp, true );
   }
-  fe zi, x, y, xy, d2, o0, o1, o2;
-  fe_invert( zi, acc.Z );
-  fe_mul( x, acc.X, zi ); fe_mul( y, acc.Y, zi );
-  fe_const_d2( d2 );
-  fe_add_r( o0, y, x ); fe_sub_r( o1, y, x ); fe_mul( xy, x, y ); fe_mul( o2, xy, d2 );
-  uint32_t * e = btab + i * FD_BTAB_STRIDE;
-  for( int j=0; j<10; j++ ) { e[j] = o0.v[j]; e[10+j] = o1.v[j]; e[20+j] = o2.v[j]; }
+  ge_precomp o; ge_affine_precomp( o, acc );
+  uint32_t * e = btab + g * FD_BTAB_STRIDE;
+  for( int j=0; j<10; j++ ) { e[j] = o.YpX.v[j]; e[10+j] = o.YmX.v[j]; e[20+j] = o.T2d.v[j]; }
   e[30] = 0u; e[31] = 0u;
 }
 
@@ -91,9 +110,9 @@ struct verify_args {
   fd_ed25519_desc_t const * desc;
   uint64_t                  n;
   int8_t *                  out;
-  uint32_t const *          btab;      /* FD_BTAB_N * FD_BTAB_STRIDE u32 */
-  uint32_t *                atab;      /* FD_ATAB_N * FD_ATAB_WORDS * stride u32 */
-  uint64_t                  atab_stride;
+  uint32_t const *          btab;      /* FD_BTAB_WORDS u32                        */
+  uint32_t *                vtab;      /* FD_VTAB_N * FD_VTAB_WORDS * vtab_cap u32 */
+  uint64_t                  vtab_cap;  /* tables                                   */
   int                       ref_codes;
 };
 
@@ -147,41 +166,64 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
   sc_reduce512( k, dg );
 }
 
-/* A-table layout: entry e of lane g = 40 words (Y+X, Y-X, 2dT, 2Z; 10 limbs
-   each) split into a 128-byte record main[e][g][32] (one cache line, read with
-   8 x 16-B loads) and a 32-byte record tail[e][g][8] (4 lanes per line), so a
-   lane's entry is fetched with no over-read whatever entry its digit selects. */
-__device__ __forceinline__ void atab_ptrs( uint32_t const * atab, uint64_t cap, uint64_t gid, uint32_t e,
-                                           uint4 const ** m, uint4 const ** t ) {
-  uint64_t idx = (uint64_t)e * cap + gid;
-  *m = (uint4 const *)(atab + idx * 32u);
-  *t = (uint4 const *)(atab + (uint64_t)FD_ATAB_N * cap * 32u + idx * 8u);
+/* Variable-base table layout: entry e of thread t = 40 words (Y+X, Y-X,
+   2dT, 2Z; 10 limbs each) split into a 128-byte record main[e][t][32] (one
+   cache line, read with 8 x 16-B loads) and a 32-byte record tail[e][t][8]
+   (4 threads per line), so a thread's entry is fetched with no over-read
+   whatever entry its digit selects. */
+__device__ __forceinline__ void vtab_ptrs( uint32_t const * vtab, uint64_t cap, uint64_t t, uint32_t e,
+                                           uint4 const ** m, uint4 const ** tl ) {
+  uint64_t idx = (uint64_t)e * cap + t;
+  *m  = (uint4 const *)(vtab + idx * 32u);
+  *tl = (uint4 const *)(vtab + (uint64_t)FD_VTAB_N * cap * 32u + idx * 8u);
 }
 
-__device__ __forceinline__ void atab_store( uint32_t * atab, uint64_t cap, uint64_t gid, int e, ge_cached const & c ) {
+__device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint64_t t, int e, ge_cached const & c ) {
   uint32_t w[ 40 ];
 #pragma unroll
   for( int j=0; j<10; j++ ) { w[j] = c.YpX.v[j]; w[10+j] = c.YmX.v[j]; w[20+j] = c.T2d.v[j]; w[30+j] = c.Z2.v[j]; }
   uint4 const * mc; uint4 const * tc;
-  atab_ptrs( atab, cap, gid, (uint32_t)e, &mc, &tc );
-  uint4 * m = (uint4 *)mc; uint4 * t = (uint4 *)tc;
+  vtab_ptrs( vtab, cap, t, (uint32_t)e, &mc, &tc );
+  uint4 * m = (uint4 *)mc; uint4 * tl = (uint4 *)tc;
 #pragma unroll
   for( int j=0; j<8; j++ ) m[j] = make_uint4( w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
 #pragma unroll
-  for( int j=0; j<2; j++ ) t[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
+  for( int j=0; j<2; j++ ) tl[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
 }
 
-/* Table entry |d| (biased digit db = d + 8), negated when d < 0. */
-__device__ __forceinline__ void atab_load( ge_cached & c, uint32_t const * atab, uint64_t cap, uint64_t gid, uint32_t db ) {
-  bool neg = db < 8u;
-  uint32_t e = neg ? 8u - db : db - 8u;
-  uint4 const * m; uint4 const * t;
-  atab_ptrs( atab, cap, gid, e, &m, &t );
-  uint32_t w[ 40 ];
+/* Table [0..8](-Q) for an affine Q (Z = 1), cached form (replaces the
+   reference's -A table of fd_ed25519_double_scalar_mul_base,
+   fd_curve25519.c:136-144, and the neg of fd_ed25519_user.c:215). */
+__device__ __forceinline__ void vtab_build( uint32_t * vtab, uint64_t cap, uint64_t t, ge_p3 const & Q ) {
+  ge_p3 nQ = Q;
+  { fe x; fe_neg( x, Q.X ); fe_carry( nQ.X, x ); fe_neg( x, Q.T ); fe_carry( nQ.T, x ); }
+  ge_cached c;
+  ge_p3 id; ge_identity( id );
+  ge_to_cached( c, id );  vtab_store( vtab, cap, t, 0, c );
+  ge_to_cached( c, nQ );  vtab_store( vtab, cap, t, 1, c );
+  ge_precomp nQp;
+  { fe d2; fe_const_d2( d2 ); fe_add_r( nQp.YpX, nQ.Y, nQ.X ); fe_sub_r( nQp.YmX, nQ.Y, nQ.X ); fe_mul( nQp.T2d, nQ.T, d2 ); }
+  FE_FENCE();
+  ge_p3 P;
+  ge_dbl( P, nQ, true ); ge_to_cached( c, P ); vtab_store( vtab, cap, t, 2, c );
+#pragma unroll 1
+  for( int e=3; e<=8; e++ ) { ge_madd( P, P, nQp, true ); ge_to_cached( c, P ); vtab_store( vtab, cap, t, e, c ); FE_FENCE(); }
+}
+
+/* Issue the loads of entry |d| (biased digit db = d + 8) into raw words;
+   vtab_finish (at the use point) applies the sign. */
+__device__ __forceinline__ void vtab_fetch( uint32_t w[ 40 ], uint32_t const * vtab, uint64_t cap, uint64_t t, uint32_t db ) {
+  uint32_t e = min( db < 8u ? 8u - db : db - 8u, 8u );
+  uint4 const * m; uint4 const * tl;
+  vtab_ptrs( vtab, cap, t, e, &m, &tl );
 #pragma unroll
   for( int j=0; j<8; j++ ) { uint4 v = m[j]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
 #pragma unroll
-  for( int j=0; j<2; j++ ) { uint4 v = t[j]; w[32+4*j] = v.x; w[33+4*j] = v.y; w[34+4*j] = v.z; w[35+4*j] = v.w; }
+  for( int j=0; j<2; j++ ) { uint4 v = tl[j]; w[32+4*j] = v.x; w[33+4*j] = v.y; w[34+4*j] = v.z; w[35+4*j] = v.w; }
+}
+
+__device__ __forceinline__ void vtab_finish( ge_cached & c, uint32_t const w[ 40 ], uint32_t db ) {
+  bool neg = db < 8u;
   fe tv, tn;
 #pragma unroll
   for( int j=0; j<10; j++ ) { tv.v[j] = w[20+j]; c.Z2.v[j] = w[30+j]; }
@@ -213,118 +255,197 @@ __device__ __forceinline__ void btab_load( ge_precomp & q, uint32_t const * lds_
   }
 }
 
+/* acc = [u](-A) + [v](-R) + [w_lo]B + [w_hi](2^128 B) over nw 4-bit windows
+   (wave-uniform; one shared doubling chain -- Straus).  u / v digits from
+   LDS rows (biased by 8, sign of u folded in), w digits (biased by 128)
+   at every other window.  Table entries are fetched one step ahead: A's for
+   the next window before the doublings, R's before A's addition. */
+__device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, uint64_t cap, uint64_t ta, uint64_t tr,
+                                          uint8_t const * dig, uint32_t const * lds_bt, int nw ) {
+  ge_identity( acc );
+  uint32_t raw[ 40 ];
+  uint32_t dba = dig[ (FD_ROW_U + nw-1)*FD_VERIFY_BLOCK ];
+  vtab_fetch( raw, vtab, cap, ta, dba );
+#pragma unroll 1
+  for( int i=nw-1; i>=0; i-- ) {
+    if( i < nw-1 ) {
+#pragma unroll 1
+      for( int j=0; j<4; j++ ) { ge_dbl( acc, acc, j == 3 ); FE_FENCE(); }
+    }
+    bool bq = ((i & 1) == 0) && (i <= 30);
+    ge_cached q;
+    vtab_finish( q, raw, dba );
+    uint32_t dbr = dig[ (FD_ROW_V + i)*FD_VERIFY_BLOCK ];
+    vtab_fetch( raw, vtab, cap, tr, dbr );
+    FE_FENCE();
+    ge_add_cached( acc, acc, q, true );
+    FE_FENCE();
+    vtab_finish( q, raw, dbr );
+    if( i > 0 ) { dba = dig[ (FD_ROW_U + i-1)*FD_VERIFY_BLOCK ]; vtab_fetch( raw, vtab, cap, ta, dba ); }
+    FE_FENCE();
+    ge_add_cached( acc, acc, q, bq );
+    FE_FENCE();
+    if( bq ) {
+      ge_precomp bp;
+      btab_load( bp, lds_bt, dig[ (FD_ROW_W + (i>>1))*FD_VERIFY_BLOCK ] );
+      FE_FENCE();
+      ge_madd( acc, acc, bp, true );
+      FE_FENCE();
+      btab_load( bp, lds_bt + FD_BTAB_N*FD_BTAB_STRIDE, dig[ (FD_ROW_W + 16 + (i>>1))*FD_VERIFY_BLOCK ] );
+      FE_FENCE();
+      ge_madd( acc, acc, bp, false );
+      FE_FENCE();
+    }
+  }
+}
+
+__device__ __forceinline__ int bitlen8( uint32_t const x[ 8 ] ) {
+  int b = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) b = x[j] ? 32*j + 32 - __clz( (int)x[j] ) : b;
+  return b;
+}
+
+/* Signed 4-bit recoding of x (< 2^(4 nw - 1)) into nw LDS rows (biased by 8,
+   negated when neg). */
+__device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 ], int neg, int nw ) {
+  int c = 0;
+#pragma unroll
+  for( int i=0; i<FD_NDIG_MAX; i++ ) {
+    if( i < nw ) {
+      int d = (int)((x[i>>3] >> (4*(i&7))) & 15u) + c;
+      c = d >= 8;
+      d -= c << 4;
+      row[ i*FD_VERIFY_BLOCK ] = (uint8_t)((neg ? -d : d) + 8);
+    }
+  }
+}
+
+/* One signature per lane:
+     S check -> k = SHA-512(R||A||M) mod l -> (u, v) short vector of k mod 8l,
+     w = v S mod l, digits -> LDS -> decode A and R, small-order checks,
+     tables [0..8](-A), [0..8](-R) -> Q = [u](-A) + [v](-R) + [w]B -> Q == O
+   (Q = [v]([S]B - [k]A - R), fd_lattice_dev.h).  The reported code follows
+   the reference's check order (fd_ed25519_user.c:157-228): S, decode A,
+   decode R, small-order A, small-order R, equation. */
 __global__ void __launch_bounds__( FD_VERIFY_BLOCK, FD_VERIFY_WAVES_PER_EU )
 fd_ed25519_verify_kernel( verify_args args ) {
-  __shared__ uint32_t s_btab[ FD_BTAB_N * FD_BTAB_STRIDE ];
-  __shared__ uint8_t  s_dig[ 96 * FD_VERIFY_BLOCK ];   /* [digit][lane]: 64 k-digits, 32 S-digits */
+  __shared__ uint4    s_btab4[ FD_BTAB_WORDS / 4 ];
+  __shared__ uint8_t  s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
 
-  for( int i=threadIdx.x; i<FD_BTAB_N*FD_BTAB_STRIDE; i+=blockDim.x ) s_btab[i] = args.btab[i];
+  int tid = (int)threadIdx.x;
+  uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)tid;
+  uint64_t cap = args.vtab_cap;
+  uint32_t const * s_btab = (uint32_t const *)s_btab4;
+  {
+    uint4 const * g = (uint4 const *)args.btab;
+    for( int i=tid; i<FD_BTAB_WORDS/4; i+=FD_VERIFY_BLOCK ) s_btab4[i] = g[i];
+  }
   __syncthreads();
 
-  uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if( gid >= args.n ) return;
-
-  fd_ed25519_desc_t d = args.desc[ gid ];
+  /* Every lane stays to the wave-wide window count below (no early exit):
+     lanes past n or with a bad descriptor take the no-work path. */
+  bool valid = gid < args.n;
+  fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
+  if( valid ) d = args.desc[ gid ];
   uint64_t asz = args.arena_sz;
-  if( (uint64_t)d.sig_off + 64u > asz || (uint64_t)d.pub_off + 32u > asz || (uint64_t)d.msg_off + d.msg_sz > asz ) {
-    args.out[ gid ] = (int8_t)FD_ED25519_GPU_CODE_BAD_DESC;
-    return;
-  }
+  bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
+                 (uint64_t)d.msg_off + d.msg_sz <= asz;
   uint32_t lim_dw = (uint32_t)((asz + 3u) >> 2) + 1u;   /* last readable dword (arena padded by 8 bytes) */
 
   uint32_t sig[ 16 ], pub[ 8 ];
-  load_words<16>( sig, args.arena, d.sig_off, lim_dw );
-  load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
+#pragma unroll
+  for( int j=0; j<16; j++ ) sig[j] = 0u;
+#pragma unroll
+  for( int j=0; j<8; j++ ) pub[j] = 0u;
+  if( desc_ok ) {
+    load_words<16>( sig, args.arena, d.sig_off, lim_dw );
+    load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
+  }
+  bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                           /* :157-159 */
+  bool live  = desc_ok && !bad_s;
 
-  /* Work is ordered to keep few values live (hash first, then A -> table,
-     then R); the reported code follows the reference's check order
-     (fd_ed25519_user.c:157-198): S, decode A, decode R, small-order A,
-     small-order R, then the group equation. */
-  bool bad_s = !sc_lt_l( sig + 8 );                                      /* :157-159 */
-  uint8_t * dig = s_dig + threadIdx.x;
-  if( !bad_s ) {
-    uint32_t k[ 8 ];
-    hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );    /* :203-206 */
-    uint8_t dk[ 64 ], ds[ 32 ];
-    sc_recode_w4( dk, k );
-    sc_recode_w8( ds, sig + 8 );
+  /* k, lattice vector, w and digits (before the decodes: only digits stay live) */
+  uint8_t * drow = s_dig + tid;
+  {
+    uint32_t u[ 8 ], v[ 8 ];
+    int un = 0, nbits = 0;
 #pragma unroll
-    for( int i=0; i<64; i++ ) dig[ i*FD_VERIFY_BLOCK ] = dk[i];
+    for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; }
+    if( live ) {
+      uint32_t k[ 8 ];
+      hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );  /* :203-206 */
+      FE_FENCE();
+      lat_short_vector( k, u, v, &un );
+      FE_FENCE();
+      uint32_t pr[ 16 ];                                                 /* w = v S mod l */
 #pragma unroll
-    for( int i=0; i<32; i++ ) dig[ (64+i)*FD_VERIFY_BLOCK ] = ds[i];
+      for( int j=0; j<16; j++ ) pr[j] = 0u;
+#pragma unroll
+      for( int i=0; i<8; i++ ) {
+        uint64_t c = 0;
+#pragma unroll
+        for( int j=0; j<8; j++ ) { uint64_t t = (uint64_t)v[i] * sig[8+j] + pr[i+j] + c; pr[i+j] = (uint32_t)t; c = t >> 32; }
+        pr[i+8] = (uint32_t)c;
+      }
+      uint32_t w[ 8 ];
+      sc_reduce512( w, pr );
+      uint8_t ds[ 32 ];
+      sc_recode_w8( ds, w );
+#pragma unroll
+      for( int i=0; i<32; i++ ) drow[ (FD_ROW_W + i)*FD_VERIFY_BLOCK ] = ds[i];
+      nbits = max( bitlen8( u ), bitlen8( v ) );
+    }
+    /* wave-uniform window count: x < 2^(4 nw - 1) for every lane's u, v */
+#pragma unroll
+    for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
+    int nw = min( FD_NDIG_MAX, max( 32, (nbits + 4) >> 2 ) );
+    recode4_lds( drow + FD_ROW_U*FD_VERIFY_BLOCK, u, un, nw );
+    recode4_lds( drow + FD_ROW_V*FD_VERIFY_BLOCK, v, 0,  nw );
+    if( (tid & 63) == 0 ) drow[ FD_ROW_NW*FD_VERIFY_BLOCK ] = (uint8_t)nw;
   }
   FE_FENCE();
 
-  uint64_t stride = args.atab_stride;
-  bool okA = false, smallA = false;
-  if( !bad_s ) {
-    ge_p3 A;
-    okA = ge_decode( A, pub, !args.ref_codes );                          /* :162 frombytes_2x */
-    smallA = ge_affine_small_order( A );                                 /* :193-195 */
-    FE_FENCE();
-    if( okA && !smallA ) {
-      /* table of [0..8](-A), cached form (:215 neg, :136-144 table) */
-      ge_p3 nA = A;
-      { fe t; fe_neg( t, A.X ); fe_carry( nA.X, t ); fe_neg( t, A.T ); fe_carry( nA.T, t ); }
-      ge_cached c;
-      ge_p3 id; ge_identity( id );
-      ge_to_cached( c, id );  atab_store( args.atab, stride, gid, 0, c );
-      ge_to_cached( c, nA );  atab_store( args.atab, stride, gid, 1, c );
-      ge_precomp nAp;
-      { fe d2; fe_const_d2( d2 ); fe_add_r( nAp.YpX, nA.Y, nA.X ); fe_sub_r( nAp.YmX, nA.Y, nA.X ); fe_mul( nAp.T2d, nA.T, d2 ); }
-      FE_FENCE();
-      ge_p3 P;
-      ge_dbl( P, nA, true ); ge_to_cached( c, P ); atab_store( args.atab, stride, gid, 2, c );
+  /* decode A then R (:162 frombytes_2x), small order (:193-198), tables */
+  int st[ 2 ] = { 0, 0 };
+  if( live ) {
 #pragma unroll 1
-      for( int e=3; e<=8; e++ ) { ge_madd( P, P, nAp, true ); ge_to_cached( c, P ); atab_store( args.atab, stride, gid, e, c ); FE_FENCE(); }
+    for( int q=0; q<2; q++ ) {
+      uint32_t enc[ 8 ];
+#pragma unroll
+      for( int j=0; j<8; j++ ) enc[j] = q ? sig[j] : pub[j];
+      ge_p3 Q;
+      int ok = ge_decode( Q, enc, !args.ref_codes );
+      int sm = ge_affine_small_order( Q );
+      FE_FENCE();
+      if( ok && !sm ) vtab_build( args.vtab, cap, (uint64_t)q*cap/2u + gid, Q );
+      int s = (ok ? 1 : 0) | (sm ? 2 : 0);
+      if( q ) st[1] = s; else st[0] = s;
+      FE_FENCE();
     }
   }
-  FE_FENCE();
+  int stA = st[0], stR = st[1];
 
-  bool okR = false, smallR = false;
-  fe xR, yR;
-  if( !bad_s ) {
-    ge_p3 R;
-    okR = ge_decode( R, sig, !args.ref_codes );
-    smallR = ge_affine_small_order( R );                                 /* :196-198 */
-    xR = R.X; yR = R.Y;
-  }
-  FE_FENCE();
-
+  if( !valid ) return;
   int code;
-  if     ( bad_s  ) code = FD_ED25519_ERR_SIG;
-  else if( !okA   ) code = args.ref_codes ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;   /* :190-192 */
-  else if( !okR   ) code = FD_ED25519_ERR_SIG;
-  else if( smallA ) code = FD_ED25519_ERR_PUBKEY;
-  else if( smallR ) code = FD_ED25519_ERR_SIG;
-  else              code = 0;
+  if     ( !desc_ok    ) code = FD_ED25519_GPU_CODE_BAD_DESC;
+  else if( bad_s       ) code = FD_ED25519_ERR_SIG;
+  else if( !(stA & 1)  ) code = args.ref_codes ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;   /* :190-192 */
+  else if( !(stR & 1)  ) code = FD_ED25519_ERR_SIG;
+  else if( stA & 2     ) code = FD_ED25519_ERR_PUBKEY;                                        /* :193-195 */
+  else if( stR & 2     ) code = FD_ED25519_ERR_SIG;                                           /* :196-198 */
+  else                   code = 0;
 
   if( code == 0 ) {
-    /* [k](-A) + [S]B  (replaces fd_ed25519_double_scalar_mul_base, fd_curve25519.c:122-166) */
-    ge_p3 acc; ge_identity( acc );
-#pragma unroll 1
-    for( int i=63; i>=0; i-- ) {
-      /* 4 doublings as a real loop: the unrolled body (4 x ~3k instructions)
-         overflows the 64 KB instruction cache shared by a CU pair and a lone
-         wave per SIMD then stalls on instruction fetch. */
-#pragma unroll 1
-      for( int j=(i < 63 ? 0 : 4); j<4; j++ ) { ge_dbl( acc, acc, j == 3 ); FE_FENCE(); }
-      ge_cached q;
-      atab_load( q, args.atab, stride, gid, dig[ i*FD_VERIFY_BLOCK ] );
-      bool even = (i & 1) == 0;
-      FE_FENCE();
-      ge_add_cached( acc, acc, q, even );
-      FE_FENCE();
-      if( even ) {
-        ge_precomp bq;
-        btab_load( bq, s_btab, dig[ (64 + (i>>1))*FD_VERIFY_BLOCK ] );
-        FE_FENCE();
-        ge_madd( acc, acc, bq, false );
-        FE_FENCE();
-      }
-    }
-    ge_p3 Rp; Rp.X = xR; Rp.Y = yR;
-    code = ge_eq_z1( acc, Rp ) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;   /* :225-228 */
+    int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
+    ge_p3 acc;
+    dsm_loop( acc, args.vtab, cap, gid, cap/2u + gid, drow, s_btab, nw );
+    /* Q == O  <=>  X == 0 and Y == Z (the reference's projective compare, :225-228, on [v]D) */
+    fe dl;
+    int ex = fe_is_zero( acc.X );
+    fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
+    int ey = fe_is_zero( dl );
+    code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
   }
   args.out[ gid ] = (int8_t)code;
 }
@@ -338,8 +459,9 @@ struct fd_dev_state {
   hipStream_t  stream;
   hipEvent_t   done;
   uint32_t *   btab;        /* device */
-  uint32_t *   atab;        /* device, FD_ATAB_N*FD_ATAB_WORDS*atab_cap u32 */
-  uint64_t     atab_cap;    /* lanes */
+  uint32_t *   vtab;        /* device, FD_VTAB_N*FD_VTAB_WORDS*vtab_cap u32 */
+  uint64_t     vtab_cap;    /* tables (2 per signature) */
+  uint64_t     sig_cap;     /* signatures per launch     */
   uint8_t *    d_arena;  uint64_t arena_cap;
   fd_ed25519_desc_t * d_desc; uint64_t desc_cap;
   int8_t *     d_out;
@@ -386,11 +508,11 @@ static int dev_reserve( fd_dev_state * s, uint64_t arena_sz, uint64_t cnt ) {
 static int dev_launch( fd_ed25519_gpu_t * ctx, fd_dev_state * s, uint8_t const * d_arena, uint64_t arena_sz,
                        fd_ed25519_desc_t const * d_desc, uint64_t cnt, int8_t * d_out, hipStream_t st ) {
   HIPCK( hipSetDevice( s->dev ) );
-  for( uint64_t off=0; off<cnt; off+=s->atab_cap ) {
-    uint64_t m = cnt - off < s->atab_cap ? cnt - off : s->atab_cap;
+  for( uint64_t off=0; off<cnt; off+=s->sig_cap ) {
+    uint64_t m = cnt - off < s->sig_cap ? cnt - off : s->sig_cap;
     verify_args a;
     a.arena = d_arena; a.arena_sz = arena_sz; a.desc = d_desc + off; a.n = m; a.out = d_out + off;
-    a.btab = s->btab; a.atab = s->atab; a.atab_stride = s->atab_cap; a.ref_codes = ctx->ref_codes;
+    a.btab = s->btab; a.vtab = s->vtab; a.vtab_cap = s->vtab_cap; a.ref_codes = ctx->ref_codes;
     uint32_t blocks = (uint32_t)((m + FD_VERIFY_BLOCK - 1u) / FD_VERIFY_BLOCK);
     hipLaunchKernelGGL( fd_ed25519_verify_kernel, dim3( blocks ), dim3( FD_VERIFY_BLOCK ), 0, st, a );
     HIPCK( hipGetLastError() );
@@ -416,11 +538,12 @@ fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch ) {
     if( hipSetDevice( i ) != hipSuccess ) goto fail;
     if( hipStreamCreateWithFlags( &s->stream, hipStreamNonBlocking ) != hipSuccess ) goto fail;
     if( hipEventCreateWithFlags( &s->done, hipEventDisableTiming ) != hipSuccess ) goto fail;
-    if( hipMalloc( &s->btab, FD_BTAB_N * FD_BTAB_STRIDE * sizeof(uint32_t) ) != hipSuccess ) goto fail;
-    s->atab_cap = align_up( max_batch, FD_VERIFY_BLOCK );
-    if( hipMalloc( &s->atab, (uint64_t)FD_ATAB_N * FD_ATAB_WORDS * s->atab_cap * sizeof(uint32_t) ) != hipSuccess ) goto fail;
+    if( hipMalloc( &s->btab, FD_BTAB_WORDS * sizeof(uint32_t) ) != hipSuccess ) goto fail;
+    s->sig_cap  = align_up( max_batch, FD_VERIFY_BLOCK );
+    s->vtab_cap = 2u * s->sig_cap;   /* tables of -A at [0, sig_cap), of -R at [sig_cap, 2 sig_cap) */
+    if( hipMalloc( &s->vtab, (uint64_t)FD_VTAB_N * FD_VTAB_WORDS * s->vtab_cap * sizeof(uint32_t) ) != hipSuccess ) goto fail;
     ctx->ndev++;
-    hipLaunchKernelGGL( fd_ed25519_btab_init, dim3( 1 ), dim3( 256 ), 0, s->stream, s->btab );
+    hipLaunchKernelGGL( fd_ed25519_btab_init, dim3( (2*FD_BTAB_N + 63)/64 ), dim3( 64 ), 0, s->stream, s->btab );
     if( hipStreamSynchronize( s->stream ) != hipSuccess ) goto fail;
   }
   if( !ctx->ndev ) goto fail;
@@ -439,7 +562,7 @@ fd_ed25519_gpu_delete( fd_ed25519_gpu_t * ctx ) {
     hipSetDevice( s->dev );
     if( s->stream ) hipStreamSynchronize( s->stream );
     if( s->btab )    hipFree( s->btab );
-    if( s->atab )    hipFree( s->atab );
+    if( s->vtab )    hipFree( s->vtab );
     if( s->d_arena ) hipFree( s->d_arena );
     if( s->d_desc )  hipFree( s->d_desc );
     if( s->d_out )   hipFree( s->d_out );

@@ -46,49 +46,15 @@ struct fe { uint32_t v[ 10 ]; };
 #define FE_2PE  (2u*0x3ffffffu)
 #define FE_2PO  (2u*0x1ffffffu)
 
-/* 32x32->64 multiply-accumulate chains.  On the device each column of a
-   product is ONE inline-asm block of dependent v_mad_u64_u32 (carry-out to
-   vcc, discarded): the compiler can neither re-associate the chain into
-   parallel partial sums (an extra 64-bit add per column and ~30 VGPRs) nor
-   pad each single-instruction asm statement with an s_nop, which its inline
-   asm hazard check does between back-to-back asm statements.  A dependent
-   v_mad_u64_u32 chain was measured to issue at the rate of independent ones
-   (tools/valu_probe.hip, ILP 1 vs 12). */
-#if defined(__HIP_DEVICE_COMPILE__)
-FD_FN uint64_t mad64( uint32_t a, uint32_t b, uint64_t c ) {
-  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b) : "vcc" );
-  return c;
-}
-FD_FN uint64_t col5( uint64_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2,
-                     uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4 ) {
-  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %0\n\t"
-       "v_mad_u64_u32 %0, vcc, %3, %4, %0\n\t"
-       "v_mad_u64_u32 %0, vcc, %5, %6, %0\n\t"
-       "v_mad_u64_u32 %0, vcc, %7, %8, %0\n\t"
-       "v_mad_u64_u32 %0, vcc, %9, %10, %0"
-       : "+v"(c) : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4) : "vcc" );
-  return c;
-}
-#else
+/* 32x32->64 multiply-accumulate (host path and single uses on the device,
+   where the compiler emits one v_mad_u64_u32). */
 FD_FN uint64_t mad64( uint32_t a, uint32_t b, uint64_t c ) { return (uint64_t)a * (uint64_t)b + c; }
 FD_FN uint64_t col5( uint64_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2,
                      uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4 ) {
   return c + (uint64_t)a0*b0 + (uint64_t)a1*b1 + (uint64_t)a2*b2 + (uint64_t)a3*b3 + (uint64_t)a4*b4;
 }
-#endif
-#if defined(__HIP_DEVICE_COMPILE__)
-#define COL10( c, a0,b0,a1,b1,a2,b2,a3,b3,a4,b4,a5,b5,a6,b6,a7,b7,a8,b8,a9,b9 ) ({ uint64_t _c = (c); \
-  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %0\n\tv_mad_u64_u32 %0, vcc, %3, %4, %0\n\t"         \
-       "v_mad_u64_u32 %0, vcc, %5, %6, %0\n\tv_mad_u64_u32 %0, vcc, %7, %8, %0\n\t"         \
-       "v_mad_u64_u32 %0, vcc, %9, %10, %0\n\tv_mad_u64_u32 %0, vcc, %11, %12, %0\n\t"      \
-       "v_mad_u64_u32 %0, vcc, %13, %14, %0\n\tv_mad_u64_u32 %0, vcc, %15, %16, %0\n\t"     \
-       "v_mad_u64_u32 %0, vcc, %17, %18, %0\n\tv_mad_u64_u32 %0, vcc, %19, %20, %0"           \
-       : "+v"(_c) : "v"(a0),"v"(b0),"v"(a1),"v"(b1),"v"(a2),"v"(b2),"v"(a3),"v"(b3),"v"(a4),"v"(b4), \
-                    "v"(a5),"v"(b5),"v"(a6),"v"(b6),"v"(a7),"v"(b7),"v"(a8),"v"(b8),"v"(a9),"v"(b9) : "vcc" ); _c; })
-#else
 #define COL10( c, a0,b0,a1,b1,a2,b2,a3,b3,a4,b4,a5,b5,a6,b6,a7,b7,a8,b8,a9,b9 ) \
   col5( col5( (c), a0,b0,a1,b1,a2,b2,a3,b3,a4,b4 ), a5,b5,a6,b6,a7,b7,a8,b8,a9,b9 )
-#endif
 
 /* Scheduling fence: keeps the machine scheduler from interleaving
    independent field products (which raises VGPR pressure past the
@@ -138,6 +104,224 @@ FD_FN void fe_neg( fe & r, fe const & a ) {
    into the next column's accumulator. */
 #define FE_COL_DONE( acc, out, sh, msk ) do { (out) = (uint32_t)(acc) & (msk); (acc) = (acc) >> (sh); } while( 0 )
 
+#if defined(__HIP_DEVICE_COMPILE__)
+/* h = f*g.  Inputs in M, output in R.  Device: the whole 100-MAC product is
+   ONE inline-asm block (one v_mad_u64_u32 per MAC, each column's 64-bit
+   accumulator seeded with the previous column's carry by one
+   v_lshrrev_b64), so the compiler pads it with a single s_nop instead of
+   one per column, and cannot re-associate the chains. */
+FD_FN void fe_mul( fe & h, fe const & f, fe const & g ) {
+  uint32_t f0=f.v[0],f1=f.v[1],f2=f.v[2],f3=f.v[3],f4=f.v[4],f5=f.v[5],f6=f.v[6],f7=f.v[7],f8=f.v[8],f9=f.v[9];
+  uint32_t g0=g.v[0],g1=g.v[1],g2=g.v[2],g3=g.v[3],g4=g.v[4],g5=g.v[5],g6=g.v[6],g7=g.v[7],g8=g.v[8],g9=g.v[9];
+  uint32_t g1_19=19u*g1, g2_19=19u*g2, g3_19=19u*g3, g4_19=19u*g4, g5_19=19u*g5;
+  uint32_t g6_19=19u*g6, g7_19=19u*g7, g8_19=19u*g8, g9_19=19u*g9;
+  uint32_t f1_2=2u*f1, f3_2=2u*f3, f5_2=2u*f5, f7_2=2u*f7, f9_2=2u*f9;
+  uint64_t c0,c1,c2,c3,c4,c5,c6,c7,c8,c9;
+  asm( "v_mad_u64_u32 %0, vcc, %10, %20, 0\n\t"
+       "v_mad_u64_u32 %0, vcc, %39, %38, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %12, %37, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %40, %36, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %14, %35, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %41, %34, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %16, %33, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %42, %32, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %18, %31, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %43, %30, %0\n\t"
+       "v_lshrrev_b64 %1, 26, %0\n\t"
+       "v_mad_u64_u32 %1, vcc, %10, %21, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %11, %20, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %12, %38, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %13, %37, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %14, %36, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %15, %35, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %16, %34, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %17, %33, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %18, %32, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %19, %31, %1\n\t"
+       "v_lshrrev_b64 %2, 25, %1\n\t"
+       "v_mad_u64_u32 %2, vcc, %10, %22, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %39, %21, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %12, %20, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %40, %38, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %14, %37, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %41, %36, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %16, %35, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %42, %34, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %18, %33, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %43, %32, %2\n\t"
+       "v_lshrrev_b64 %3, 26, %2\n\t"
+       "v_mad_u64_u32 %3, vcc, %10, %23, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %11, %22, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %12, %21, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %13, %20, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %14, %38, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %15, %37, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %16, %36, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %17, %35, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %18, %34, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %19, %33, %3\n\t"
+       "v_lshrrev_b64 %4, 25, %3\n\t"
+       "v_mad_u64_u32 %4, vcc, %10, %24, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %39, %23, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %12, %22, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %40, %21, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %14, %20, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %41, %38, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %16, %37, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %42, %36, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %18, %35, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %43, %34, %4\n\t"
+       "v_lshrrev_b64 %5, 26, %4\n\t"
+       "v_mad_u64_u32 %5, vcc, %10, %25, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %11, %24, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %12, %23, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %13, %22, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %14, %21, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %15, %20, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %16, %38, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %17, %37, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %18, %36, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %19, %35, %5\n\t"
+       "v_lshrrev_b64 %6, 25, %5\n\t"
+       "v_mad_u64_u32 %6, vcc, %10, %26, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %39, %25, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %12, %24, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %40, %23, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %14, %22, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %41, %21, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %16, %20, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %42, %38, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %18, %37, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %43, %36, %6\n\t"
+       "v_lshrrev_b64 %7, 26, %6\n\t"
+       "v_mad_u64_u32 %7, vcc, %10, %27, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %11, %26, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %12, %25, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %13, %24, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %14, %23, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %15, %22, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %16, %21, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %17, %20, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %18, %38, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %19, %37, %7\n\t"
+       "v_lshrrev_b64 %8, 25, %7\n\t"
+       "v_mad_u64_u32 %8, vcc, %10, %28, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %39, %27, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %12, %26, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %40, %25, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %14, %24, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %41, %23, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %16, %22, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %42, %21, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %18, %20, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %43, %38, %8\n\t"
+       "v_lshrrev_b64 %9, 26, %8\n\t"
+       "v_mad_u64_u32 %9, vcc, %10, %29, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %11, %28, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %12, %27, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %13, %26, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %14, %25, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %15, %24, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %16, %23, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %17, %22, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %18, %21, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %19, %20, %9"
+       : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3), "=&v"(c4), "=&v"(c5), "=&v"(c6), "=&v"(c7), "=&v"(c8), "=&v"(c9)
+       : "v"(f0), "v"(f1), "v"(f2), "v"(f3), "v"(f4), "v"(f5), "v"(f6), "v"(f7), "v"(f8), "v"(f9), "v"(g0), "v"(g1), "v"(g2), "v"(g3), "v"(g4), "v"(g5), "v"(g6), "v"(g7), "v"(g8), "v"(g9), "v"(g1_19), "v"(g2_19), "v"(g3_19), "v"(g4_19), "v"(g5_19), "v"(g6_19), "v"(g7_19), "v"(g8_19), "v"(g9_19), "v"(f1_2), "v"(f3_2), "v"(f5_2), "v"(f7_2), "v"(f9_2) : "vcc" );
+  uint32_t h0 = (uint32_t)c0 & FE_M26, h1 = (uint32_t)c1 & FE_M25, h2 = (uint32_t)c2 & FE_M26, h3 = (uint32_t)c3 & FE_M25;
+  uint32_t h4 = (uint32_t)c4 & FE_M26, h5 = (uint32_t)c5 & FE_M25, h6 = (uint32_t)c6 & FE_M26, h7 = (uint32_t)c7 & FE_M25;
+  uint32_t h8 = (uint32_t)c8 & FE_M26, h9 = (uint32_t)c9 & FE_M25;
+  uint64_t a = c9 >> 25;
+  /* a = carry out of limb 9 (< 2^38): times 19 back into limb 0 */
+  a = mad64( (uint32_t)a, 19u, (uint64_t)h0 ) + ((uint64_t)(19u*(uint32_t)(a>>32))<<32);
+  h0 = (uint32_t)a & FE_M26;
+  h1 += (uint32_t)(a >> 26);
+  h.v[0]=h0; h.v[1]=h1; h.v[2]=h2; h.v[3]=h3; h.v[4]=h4; h.v[5]=h5; h.v[6]=h6; h.v[7]=h7; h.v[8]=h8; h.v[9]=h9;
+}
+
+/* h = f^2.  Input in M, output in R (55 MACs, one asm block). */
+FD_FN void fe_sq( fe & h, fe const & f ) {
+  uint32_t f0=f.v[0],f1=f.v[1],f2=f.v[2],f3=f.v[3],f4=f.v[4],f5=f.v[5],f6=f.v[6],f7=f.v[7],f8=f.v[8],f9=f.v[9];
+  uint32_t f0_2=2u*f0, f1_2=2u*f1, f2_2=2u*f2, f3_2=2u*f3, f4_2=2u*f4, f5_2=2u*f5, f6_2=2u*f6, f7_2=2u*f7;
+  uint32_t f5_38=38u*f5, f6_19=19u*f6, f7_38=38u*f7, f8_19=19u*f8, f9_38=38u*f9;
+  uint64_t c0,c1,c2,c3,c4,c5,c6,c7,c8,c9;
+  asm( "v_mad_u64_u32 %0, vcc, %10, %10, 0\n\t"
+       "v_mad_u64_u32 %0, vcc, %21, %32, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %22, %31, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %23, %30, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %24, %29, %0\n\t"
+       "v_mad_u64_u32 %0, vcc, %15, %28, %0\n\t"
+       "v_lshrrev_b64 %1, 26, %0\n\t"
+       "v_mad_u64_u32 %1, vcc, %20, %11, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %12, %32, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %23, %31, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %14, %30, %1\n\t"
+       "v_mad_u64_u32 %1, vcc, %25, %29, %1\n\t"
+       "v_lshrrev_b64 %2, 25, %1\n\t"
+       "v_mad_u64_u32 %2, vcc, %21, %11, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %23, %32, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %24, %31, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %25, %30, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %16, %29, %2\n\t"
+       "v_mad_u64_u32 %2, vcc, %20, %12, %2\n\t"
+       "v_lshrrev_b64 %3, 26, %2\n\t"
+       "v_mad_u64_u32 %3, vcc, %20, %13, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %21, %12, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %14, %32, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %25, %31, %3\n\t"
+       "v_mad_u64_u32 %3, vcc, %16, %30, %3\n\t"
+       "v_lshrrev_b64 %4, 25, %3\n\t"
+       "v_mad_u64_u32 %4, vcc, %21, %23, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %12, %12, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %25, %32, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %26, %31, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %17, %30, %4\n\t"
+       "v_mad_u64_u32 %4, vcc, %20, %14, %4\n\t"
+       "v_lshrrev_b64 %5, 26, %4\n\t"
+       "v_mad_u64_u32 %5, vcc, %20, %15, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %21, %14, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %22, %13, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %16, %32, %5\n\t"
+       "v_mad_u64_u32 %5, vcc, %27, %31, %5\n\t"
+       "v_lshrrev_b64 %6, 25, %5\n\t"
+       "v_mad_u64_u32 %6, vcc, %21, %25, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %22, %14, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %23, %13, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %27, %32, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %18, %31, %6\n\t"
+       "v_mad_u64_u32 %6, vcc, %20, %16, %6\n\t"
+       "v_lshrrev_b64 %7, 26, %6\n\t"
+       "v_mad_u64_u32 %7, vcc, %20, %17, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %21, %16, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %22, %15, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %23, %14, %7\n\t"
+       "v_mad_u64_u32 %7, vcc, %18, %32, %7\n\t"
+       "v_lshrrev_b64 %8, 25, %7\n\t"
+       "v_mad_u64_u32 %8, vcc, %21, %27, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %22, %16, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %23, %25, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %14, %14, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %19, %32, %8\n\t"
+       "v_mad_u64_u32 %8, vcc, %20, %18, %8\n\t"
+       "v_lshrrev_b64 %9, 26, %8\n\t"
+       "v_mad_u64_u32 %9, vcc, %20, %19, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %21, %18, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %22, %17, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %23, %16, %9\n\t"
+       "v_mad_u64_u32 %9, vcc, %24, %15, %9"
+       : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3), "=&v"(c4), "=&v"(c5), "=&v"(c6), "=&v"(c7), "=&v"(c8), "=&v"(c9)
+       : "v"(f0), "v"(f1), "v"(f2), "v"(f3), "v"(f4), "v"(f5), "v"(f6), "v"(f7), "v"(f8), "v"(f9), "v"(f0_2), "v"(f1_2), "v"(f2_2), "v"(f3_2), "v"(f4_2), "v"(f5_2), "v"(f6_2), "v"(f7_2), "v"(f5_38), "v"(f6_19), "v"(f7_38), "v"(f8_19), "v"(f9_38) : "vcc" );
+  uint32_t h0 = (uint32_t)c0 & FE_M26, h1 = (uint32_t)c1 & FE_M25, h2 = (uint32_t)c2 & FE_M26, h3 = (uint32_t)c3 & FE_M25;
+  uint32_t h4 = (uint32_t)c4 & FE_M26, h5 = (uint32_t)c5 & FE_M25, h6 = (uint32_t)c6 & FE_M26, h7 = (uint32_t)c7 & FE_M25;
+  uint32_t h8 = (uint32_t)c8 & FE_M26, h9 = (uint32_t)c9 & FE_M25;
+  uint64_t a = c9 >> 25;
+  /* a = carry out of limb 9 (< 2^38): times 19 back into limb 0 */
+  a = mad64( (uint32_t)a, 19u, (uint64_t)h0 ) + ((uint64_t)(19u*(uint32_t)(a>>32))<<32);
+  h0 = (uint32_t)a & FE_M26;
+  h1 += (uint32_t)(a >> 26);
+  h.v[0]=h0; h.v[1]=h1; h.v[2]=h2; h.v[3]=h3; h.v[4]=h4; h.v[5]=h5; h.v[6]=h6; h.v[7]=h7; h.v[8]=h8; h.v[9]=h9;
+}
+#else
 /* h = f*g.  Inputs in M, output in R. */
 FD_FN void fe_mul( fe & h, fe const & f, fe const & g ) {
   uint32_t f0=f.v[0],f1=f.v[1],f2=f.v[2],f3=f.v[3],f4=f.v[4],f5=f.v[5],f6=f.v[6],f7=f.v[7],f8=f.v[8],f9=f.v[9];
@@ -206,6 +390,8 @@ FD_FN void fe_sq( fe & h, fe const & f ) {
   h1 += (uint32_t)(a >> 26);
   h.v[0]=h0; h.v[1]=h1; h.v[2]=h2; h.v[3]=h3; h.v[4]=h4; h.v[5]=h5; h.v[6]=h6; h.v[7]=h7; h.v[8]=h8; h.v[9]=h9;
 }
+
+#endif
 
 FD_FN void fe_sqn( fe & h, fe const & f, int n ) {
   fe_sq( h, f );

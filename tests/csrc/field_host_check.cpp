@@ -20,3 +20,7 @@ void t_recode4( uint8_t * o, uint32_t const * s ) { sc_recode_w4( o, s ); }
 void t_recode8( uint8_t * o, uint32_t const * s ) { sc_recode_w8( o, s ); }
 void t_sha_block( uint64_t * h, uint64_t * w ) { sha512_compress( h, w ); }
 }
+#include "../../firedancer_amd/csrc/fd_lattice_dev.h"
+extern "C" {
+int t_lattice( uint32_t const * k, uint32_t * u, uint32_t * v, int * u_neg ) { return lat_short_vector( k, u, v, u_neg ); }
+}
