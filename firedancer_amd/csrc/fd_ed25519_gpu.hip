@@ -35,6 +35,8 @@
 #define FD_BTAB_N         129          /* [0..128]P                                   */
 #define FD_BTAB_STRIDE    32           /* u32 per entry: 3 x 10 limbs + pad           */
 #define FD_BTAB_WORDS     (2 * FD_BTAB_N * FD_BTAB_STRIDE)   /* P = B and P = 2^128 B */
+#define FD_BTAB_LOADS     ((FD_BTAB_WORDS/4 + FD_VERIFY_BLOCK - 1) / FD_VERIFY_BLOCK)   /* uint4 per thread */
+#define FD_BTAB_ALLOC     (FD_BTAB_LOADS * FD_VERIFY_BLOCK * 4)                       /* padded u32 */
 #define FD_VTAB_N         9            /* [0..8](-Q), Q = A or R                      */
 #define FD_VTAB_WORDS     40           /* u32 per entry (4 fe)                        */
 #define FD_NDIG_MAX       64           /* 4-bit windows of a <= 256-bit scalar        */
@@ -45,6 +47,16 @@
 #define FD_ROW_W          128          /* signed 8-bit digits of w = v S mod l (32)   */
 #define FD_ROW_NW         160          /* lane 0 of each wave: the wave's window count */
 #define FD_ROWS           161
+
+/* Diagnostic build only (-DFD_PHASE_STAMPS, tools/Makefile): s_memtime at
+   phase boundaries, per-wave deltas summed into args.stamps.  The product
+   build compiles none of it. */
+#ifdef FD_PHASE_STAMPS
+#define FD_NSTAMP 8
+#define STAMP( i ) do { FE_FENCE(); _st[ i ] = __builtin_amdgcn_s_memtime(); FE_FENCE(); } while( 0 )
+#else
+#define STAMP( i ) do {} while( 0 )
+#endif
 
 /* ------------------------------------------------------------------ loads */
 
@@ -114,9 +126,22 @@ struct verify_args {
   uint32_t *                vtab;      /* FD_VTAB_N * FD_VTAB_WORDS * vtab_cap u32 */
   uint64_t                  vtab_cap;  /* tables                                   */
   int                       ref_codes;
+  unsigned long long *      stamps;    /* FD_PHASE_STAMPS builds only: per-phase cycle sums */
 };
 
-/* SHA-512(R || A || M) mod l.  R, A: 8 LE words each; message streamed. */
+/* Raw message dwords of SHA block b: dword (msg_off>>2) + 32b - 16 + i,
+   i < 33, clamped to the readable arena (block 0's first 16 are unused:
+   R || A come from registers). */
+__device__ __forceinline__ void sha_fetch( uint32_t raw[ 33 ], uint32_t const * a32, uint32_t msg_off, uint32_t b,
+                                           uint32_t lim_dw ) {
+  int32_t start = (int32_t)(msg_off >> 2) + 32*(int32_t)b - 16;
+#pragma unroll
+  for( int i=0; i<33; i++ ) raw[i] = a32[ min( (uint32_t)max( start + i, 0 ), lim_dw ) ];
+}
+
+/* SHA-512(R || A || M) mod l.  R, A: 8 LE words each; the message is
+   streamed from HBM, each block's dwords fetched one block ahead so the
+   load latency hides behind the previous compression. */
 __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 ], uint32_t const Aw[ 8 ],
                                           uint8_t const * arena, uint32_t msg_off, uint32_t msg_sz, uint32_t lim_dw ) {
   uint64_t h[ 8 ]; sha512_init_state( h );
@@ -124,25 +149,25 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
   uint32_t nblk = (total + 17u + 127u) >> 7;
   uint32_t const * a32 = (uint32_t const *)arena;
   uint32_t sh = msg_off & 3u;
+  uint32_t nxt[ 33 ];
+  sha_fetch( nxt, a32, msg_off, 0u, lim_dw );
   for( uint32_t b=0; b<nblk; b++ ) {
+    uint32_t raw[ 33 ];
+#pragma unroll
+    for( int i=0; i<33; i++ ) raw[i] = nxt[i];
+    if( b + 1u < nblk ) sha_fetch( nxt, a32, msg_off, b + 1u, lim_dw );
     uint64_t W[ 16 ];
 #pragma unroll
     for( int j=0; j<16; j++ ) {
-      uint32_t s = (b << 7) + 8u*(uint32_t)j;          /* stream byte offset of this word */
       uint32_t hi, lo;                                  /* big-endian halves */
       if( b == 0 && j < 8 ) {
         uint32_t const * src = (j < 4) ? Rw : Aw;
         int jj = j & 3;
         hi = sha_bswap32( src[2*jj] ); lo = sha_bswap32( src[2*jj+1] );
       } else {
-        int32_t m = (int32_t)(s - 64u);                 /* message byte index of the word's first byte */
-        uint32_t base = msg_off + (uint32_t)m;
-        uint32_t dw = base >> 2;
-        uint32_t d0 = a32[ min( dw,      lim_dw ) ];
-        uint32_t d1 = a32[ min( dw + 1u, lim_dw ) ];
-        uint32_t d2 = a32[ min( dw + 2u, lim_dw ) ];
-        uint32_t w0 = __builtin_amdgcn_alignbyte( d1, d0, sh );   /* bytes m..m+3 LE */
-        uint32_t w1 = __builtin_amdgcn_alignbyte( d2, d1, sh );   /* bytes m+4..m+7  */
+        int32_t m = (int32_t)((b << 7) + 8u*(uint32_t)j) - 64;     /* message byte index of the word's first byte */
+        uint32_t w0 = __builtin_amdgcn_alignbyte( raw[2*j+1], raw[2*j],   sh );   /* bytes m..m+3 LE */
+        uint32_t w1 = __builtin_amdgcn_alignbyte( raw[2*j+2], raw[2*j+1], sh );   /* bytes m+4..m+7  */
         hi = sha_bswap32( w0 ); lo = sha_bswap32( w1 );
         /* padding: keep bytes < msg_sz, 0x80 at msg_sz, zeros after */
         int32_t rem0 = (int32_t)msg_sz - m;             /* valid bytes from m   */
@@ -307,14 +332,15 @@ __device__ __forceinline__ int bitlen8( uint32_t const x[ 8 ] ) {
 }
 
 /* Signed 4-bit recoding of x (< 2^(4 nw - 1)) into nw LDS rows (biased by 8,
-   negated when neg). */
+   negated when neg): digits in [-8, 7] below the top one, top digit in
+   [0, 8] (its top nibble <= 7 plus the incoming carry, never wrapped). */
 __device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 ], int neg, int nw ) {
   int c = 0;
 #pragma unroll
   for( int i=0; i<FD_NDIG_MAX; i++ ) {
     if( i < nw ) {
       int d = (int)((x[i>>3] >> (4*(i&7))) & 15u) + c;
-      c = d >= 8;
+      c = d >= 8 && i < nw-1;           /* the top digit keeps its carry: d in [0, 8] */
       d -= c << 4;
       row[ i*FD_VERIFY_BLOCK ] = (uint8_t)((neg ? -d : d) + 8);
     }
@@ -334,17 +360,17 @@ fd_ed25519_verify_kernel( verify_args args ) {
   __shared__ uint8_t  s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
 
   int tid = (int)threadIdx.x;
+#ifdef FD_PHASE_STAMPS
+  uint64_t _st[ FD_NSTAMP ] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+#endif
+  STAMP( 0 );
   uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)tid;
   uint64_t cap = args.vtab_cap;
   uint32_t const * s_btab = (uint32_t const *)s_btab4;
-  {
-    uint4 const * g = (uint4 const *)args.btab;
-    for( int i=tid; i<FD_BTAB_WORDS/4; i+=FD_VERIFY_BLOCK ) s_btab4[i] = g[i];
-  }
-  __syncthreads();
-
   /* Every lane stays to the wave-wide window count below (no early exit):
-     lanes past n or with a bad descriptor take the no-work path. */
+     lanes past n or with a bad descriptor take the no-work path.  The
+     descriptor / signature / key loads are issued before the B-table copy
+     so their latency overlaps it. */
   bool valid = gid < args.n;
   fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
   if( valid ) d = args.desc[ gid ];
@@ -362,6 +388,23 @@ fd_ed25519_verify_kernel( verify_args args ) {
     load_words<16>( sig, args.arena, d.sig_off, lim_dw );
     load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
   }
+
+  {
+    /* all of this thread's table loads in flight at once (the device copy is
+       padded to FD_BTAB_LOADS full rounds), then the LDS stores */
+    uint4 const * g = (uint4 const *)args.btab;
+    uint4 t[ FD_BTAB_LOADS ];
+#pragma unroll
+    for( int r=0; r<FD_BTAB_LOADS; r++ ) t[r] = g[ tid + r*FD_VERIFY_BLOCK ];
+#pragma unroll
+    for( int r=0; r<FD_BTAB_LOADS; r++ ) {
+      int i = tid + r*FD_VERIFY_BLOCK;
+      if( r < FD_BTAB_LOADS-1 || i < FD_BTAB_WORDS/4 ) s_btab4[i] = t[r];
+    }
+  }
+  __syncthreads();
+  STAMP( 1 );
+
   bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                           /* :157-159 */
   bool live  = desc_ok && !bad_s;
 
@@ -376,6 +419,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
       uint32_t k[ 8 ];
       hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );  /* :203-206 */
       FE_FENCE();
+      STAMP( 2 );
       lat_short_vector( k, u, v, &un );
       FE_FENCE();
       uint32_t pr[ 16 ];                                                 /* w = v S mod l */
@@ -407,6 +451,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
   FE_FENCE();
 
   /* decode A then R (:162 frombytes_2x), small order (:193-198), tables */
+  STAMP( 3 );
   int st[ 2 ] = { 0, 0 };
   if( live ) {
 #pragma unroll 1
@@ -425,6 +470,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
     }
   }
   int stA = st[0], stR = st[1];
+  STAMP( 4 );
 
   if( !valid ) return;
   int code;
@@ -440,6 +486,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
     int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
     ge_p3 acc;
     dsm_loop( acc, args.vtab, cap, gid, cap/2u + gid, drow, s_btab, nw );
+    STAMP( 5 );
     /* Q == O  <=>  X == 0 and Y == Z (the reference's projective compare, :225-228, on [v]D) */
     fe dl;
     int ex = fe_is_zero( acc.X );
@@ -448,6 +495,31 @@ fd_ed25519_verify_kernel( verify_args args ) {
     code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
   }
   args.out[ gid ] = (int8_t)code;
+#ifdef FD_PHASE_STAMPS
+  STAMP( 6 );
+  if( args.stamps && (tid & 63) == 0 ) {
+    /* 0-1 prologue+table copy, 1-2 SHA (live lanes), 2-3 lattice+digits, 3-4 decodes+tables, 4-5 loop, 5-6 tail */
+    for( int i=0; i<6; i++ ) atomicAdd( &args.stamps[i], (unsigned long long)(_st[i+1] - _st[i]) );
+    atomicAdd( &args.stamps[7], 1ull );
+  }
+#endif
+}
+
+/* Self-test kernel (tests only, fd_ed25519_gpu_test_lattice): the device
+   lattice reduction on caller-supplied k, one per lane. */
+__global__ void fd_ed25519_lattice_test_kernel( uint32_t const * k, uint32_t * out, uint64_t n ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t kk[ 8 ], u[ 8 ], v[ 8 ];
+  int un = 0, it = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) { kk[j] = i < n ? k[ i*8u + (uint64_t)j ] : 0u; u[j] = 0u; v[j] = 0u; }
+  if( i < n ) it = lat_short_vector( kk, u, v, &un );
+  if( i < n ) {
+    uint32_t * o = out + i*18u;
+#pragma unroll
+    for( int j=0; j<8; j++ ) { o[j] = u[j]; o[8+j] = v[j]; }
+    o[16] = (uint32_t)un; o[17] = (uint32_t)it;
+  }
 }
 
 /* ------------------------------------------------------------------ host side */
@@ -462,6 +534,7 @@ struct fd_dev_state {
   uint32_t *   vtab;        /* device, FD_VTAB_N*FD_VTAB_WORDS*vtab_cap u32 */
   uint64_t     vtab_cap;    /* tables (2 per signature) */
   uint64_t     sig_cap;     /* signatures per launch     */
+  unsigned long long * stamps; /* FD_PHASE_STAMPS builds only */
   uint8_t *    d_arena;  uint64_t arena_cap;
   fd_ed25519_desc_t * d_desc; uint64_t desc_cap;
   int8_t *     d_out;
@@ -513,6 +586,7 @@ static int dev_launch( fd_ed25519_gpu_t * ctx, fd_dev_state * s, uint8_t const *
     verify_args a;
     a.arena = d_arena; a.arena_sz = arena_sz; a.desc = d_desc + off; a.n = m; a.out = d_out + off;
     a.btab = s->btab; a.vtab = s->vtab; a.vtab_cap = s->vtab_cap; a.ref_codes = ctx->ref_codes;
+    a.stamps = s->stamps;
     uint32_t blocks = (uint32_t)((m + FD_VERIFY_BLOCK - 1u) / FD_VERIFY_BLOCK);
     hipLaunchKernelGGL( fd_ed25519_verify_kernel, dim3( blocks ), dim3( FD_VERIFY_BLOCK ), 0, st, a );
     HIPCK( hipGetLastError() );
@@ -538,10 +612,15 @@ fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch ) {
     if( hipSetDevice( i ) != hipSuccess ) goto fail;
     if( hipStreamCreateWithFlags( &s->stream, hipStreamNonBlocking ) != hipSuccess ) goto fail;
     if( hipEventCreateWithFlags( &s->done, hipEventDisableTiming ) != hipSuccess ) goto fail;
-    if( hipMalloc( &s->btab, FD_BTAB_WORDS * sizeof(uint32_t) ) != hipSuccess ) goto fail;
+    if( hipMalloc( &s->btab, FD_BTAB_ALLOC * sizeof(uint32_t) ) != hipSuccess ) goto fail;
+    if( hipMemsetAsync( s->btab, 0, FD_BTAB_ALLOC * sizeof(uint32_t), s->stream ) != hipSuccess ) goto fail;
     s->sig_cap  = align_up( max_batch, FD_VERIFY_BLOCK );
     s->vtab_cap = 2u * s->sig_cap;   /* tables of -A at [0, sig_cap), of -R at [sig_cap, 2 sig_cap) */
     if( hipMalloc( &s->vtab, (uint64_t)FD_VTAB_N * FD_VTAB_WORDS * s->vtab_cap * sizeof(uint32_t) ) != hipSuccess ) goto fail;
+#ifdef FD_PHASE_STAMPS
+    if( hipMalloc( &s->stamps, 8 * sizeof(unsigned long long) ) != hipSuccess ) goto fail;
+    hipMemset( s->stamps, 0, 8 * sizeof(unsigned long long) );
+#endif
     ctx->ndev++;
     hipLaunchKernelGGL( fd_ed25519_btab_init, dim3( (2*FD_BTAB_N + 63)/64 ), dim3( 64 ), 0, s->stream, s->btab );
     if( hipStreamSynchronize( s->stream ) != hipSuccess ) goto fail;
@@ -563,6 +642,17 @@ fd_ed25519_gpu_delete( fd_ed25519_gpu_t * ctx ) {
     if( s->stream ) hipStreamSynchronize( s->stream );
     if( s->btab )    hipFree( s->btab );
     if( s->vtab )    hipFree( s->vtab );
+#ifdef FD_PHASE_STAMPS
+    if( s->stamps ) {
+      unsigned long long h[ 8 ];
+      if( hipMemcpy( h, s->stamps, sizeof(h), hipMemcpyDeviceToHost ) == hipSuccess && h[7] ) {
+        char const * nm[ 6 ] = { "prologue", "sha", "lattice", "decode+tab", "loop", "tail" };
+        unsigned long long tot = 0; for( int i=0; i<6; i++ ) tot += h[i];
+        for( int i=0; i<6; i++ ) fprintf( stderr, "stamp %-10s %12.0f cyc/wave  %5.1f%%\n", nm[i], (double)h[i]/(double)h[7], 100.0*(double)h[i]/(double)tot );
+      }
+      hipFree( s->stamps );
+    }
+#endif
     if( s->d_arena ) hipFree( s->d_arena );
     if( s->d_desc )  hipFree( s->d_desc );
     if( s->d_out )   hipFree( s->d_out );
@@ -729,6 +819,25 @@ fd_ed25519_gpu_txn_reduce( int8_t const * out_code, fd_ed25519_desc_t const * de
     i = j;
   }
   return t;
+}
+
+int
+fd_ed25519_gpu_test_lattice( fd_ed25519_gpu_t * ctx, uint32_t const * k, uint64_t n, uint32_t * out ) {
+  if( !ctx || !k || !out || !n ) return FD_ED25519_GPU_ERR_ARG;
+  fd_dev_state * s = &ctx->d[0];
+  HIPCK( hipSetDevice( s->dev ) );
+  uint32_t * dk = NULL; uint32_t * dout = NULL;
+  HIPCK( hipMalloc( &dk, n * 32u ) );
+  if( hipMalloc( &dout, n * 72u ) != hipSuccess ) { hipFree( dk ); return FD_ED25519_GPU_ERR_OOM; }
+  int err = FD_ED25519_GPU_OK;
+  if( hipMemcpy( dk, k, n * 32u, hipMemcpyHostToDevice ) != hipSuccess ) err = FD_ED25519_GPU_ERR_LAUNCH;
+  if( !err ) {
+    hipLaunchKernelGGL( fd_ed25519_lattice_test_kernel, dim3( (uint32_t)((n + 255u) / 256u) ), dim3( 256 ), 0, s->stream, dk, dout, n );
+    if( hipGetLastError() != hipSuccess || hipStreamSynchronize( s->stream ) != hipSuccess ) err = FD_ED25519_GPU_ERR_LAUNCH;
+  }
+  if( !err && hipMemcpy( out, dout, n * 72u, hipMemcpyDeviceToHost ) != hipSuccess ) err = FD_ED25519_GPU_ERR_LAUNCH;
+  hipFree( dk ); hipFree( dout );
+  return err;
 }
 
 char const *

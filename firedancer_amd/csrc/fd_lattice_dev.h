@@ -156,34 +156,89 @@ FD_LT_FN int lat_any( int p ) {
 #endif
 }
 
+/* f64 approximation of x >= 2^128 from its top six words (the two low
+   words contribute < 2^-64 relative). */
+FD_LT_FN double lat_f64_hi( uint32_t const x[ 8 ] ) {
+  double f = (double)x[7];
+#pragma unroll
+  for( int j=6; j>=2; j-- ) f = fma( f, 4294967296.0, (double)x[j] );
+  return f * 18446744073709551616.0;
+}
+
+/* 1/y to ~2^-52 relative: hardware reciprocal + two Newton steps. */
+FD_LT_FN double lat_rcp( double y ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp( y );
+  r = r * fma( -y, r, 2.0 );
+  r = r * fma( -y, r, 2.0 );
+  return r;
+#else
+  return 1.0 / y;
+#endif
+}
+
+/* a < b, 8 words */
+FD_LT_FN int lat_lt( uint32_t const a[ 8 ], uint32_t const b[ 8 ] ) { return !lat_ge( a, b ); }
+
+/* One Euclid half-step on (x, tx) by (y, ty), y >= 2^128, x > y on entry:
+   x -= m y, tx += m ty with m the f64 quotient estimate (1 <= m <=
+   floor(x/y)), repeated (rarely) until x < y.  xf/yf: f64 approximations
+   of x/y on entry; xf is refreshed on exit. */
+FD_LT_FN void lat_reduce( uint32_t x[ 8 ], uint32_t tx[ 4 ], uint32_t const y[ 8 ], uint32_t const ty[ 4 ],
+                          double & xf, double yf, int act ) {
+  double ry = lat_rcp( yf );
+  double q = (xf * ry) * (1.0 - 0x1p-40);
+  int big = act && q >= 4294967296.0;
+  if( lat_any( big ) ) {
+    if( big ) {                                   /* rare: quotient >= 2^32 */
+      int s; uint32_t m = lat_qest( lat_f64( x ), lat_f64( y ), &s );
+      lat_submul<4>( x, y, tx, ty, m, s );
+    }
+  }
+  if( act && !big ) {
+    uint32_t m = q < 1.0 ? 1u : (uint32_t)q;
+    lat_submul<4>( x, y, tx, ty, m, 0 );
+  }
+  /* the estimate undershot (quotient close to an integer, or big): repeat */
+  int more = act && lat_ge( x, y );
+  while( lat_any( more ) ) {
+    if( more ) {
+      int s; uint32_t m = lat_qest( lat_f64( x ), lat_f64( y ), &s );
+      lat_submul<4>( x, y, tx, ty, m, s );
+    }
+    more = more && lat_ge( x, y );
+  }
+  if( act ) xf = lat_f64_hi( x );
+}
+
 /* Short lattice vector for k (8 LE words, k < l).  Outputs |u| and v (> 0)
-   as 8 LE words each and the sign of u.  Returns the number of loop
-   iterations (>= FD_LAT_MAX_ITER means the fallback (k, 1) was taken). */
+   as 8 LE words each and the sign of u.  Returns the number of half-steps
+   (>= FD_LAT_MAX_ITER means the fallback (k, 1) was taken).
+
+   Invariants: a tb + b ta = 8l; with the larger of (a, b) reduced by the
+   smaller in alternation (no register swap), the one just reduced is
+   r_{i+1} = (-1)^(i+1) t_{i+1} k (mod 8l) in Euclid's numbering, i.e. the
+   pair's signs alternate.  Any m in [1, floor(x/y)] keeps the invariants. */
 FD_LT_FN int lat_short_vector( uint32_t const k[ 8 ], uint32_t u[ 8 ], uint32_t v[ 8 ], int * u_neg ) {
   uint32_t a[ 8 ] = { FD_N8L0, FD_N8L1, FD_N8L2, FD_N8L3, 0u, 0u, 0u, FD_N8L7 };
   uint32_t b[ 8 ];
   uint32_t ta[ 4 ] = { 0u, 0u, 0u, 0u }, tb[ 4 ] = { 1u, 0u, 0u, 0u };
 #pragma unroll
   for( int j=0; j<8; j++ ) b[j] = k[j];
-  int par = 0;                                    /* b = (-1)^par tb k, a = -(-1)^par ta k (mod 8l) */
-  int active = (b[4] | b[5] | b[6] | b[7]) != 0u; /* b >= 2^128 */
+  /* b = +tb k, a = -ta k (mod 8l) */
+  int active = (b[4] | b[5] | b[6] | b[7]) != 0u;   /* b >= 2^128: keep going */
+  int last = 1;                                     /* which of (a, b) holds r_i: 1 = b */
   int it = 0;
+  double af = 0.0, bf = 0.0;
+  if( active ) { af = lat_f64_hi( a ); bf = lat_f64_hi( b ); }
   while( lat_any( active ) ) {
-    if( active ) {
-      if( lat_ge( a, b ) ) {
-        int s; uint32_t m = lat_qest( lat_f64( a ), lat_f64( b ), &s );
-        lat_submul<4>( a, b, ta, tb, m, s );
-      }
-      if( !lat_ge( a, b ) ) {
-#pragma unroll
-        for( int j=0; j<8; j++ ) { uint32_t x = a[j]; a[j] = b[j]; b[j] = x; }
-#pragma unroll
-        for( int j=0; j<4; j++ ) { uint32_t x = ta[j]; ta[j] = tb[j]; tb[j] = x; }
-        par ^= 1;
-      }
-      active = (b[4] | b[5] | b[6] | b[7]) != 0u;
-      if( ++it >= FD_LAT_MAX_ITER ) active = 0;
-    }
+    /* a -= q b: now a = r_{i+1} < b */
+    lat_reduce( a, ta, b, tb, af, bf, active );
+    if( active ) { last = 0; it++; active = ((a[4] | a[5] | a[6] | a[7]) != 0u) && it < FD_LAT_MAX_ITER; }
+    if( !lat_any( active ) ) break;
+    /* b -= q a */
+    lat_reduce( b, tb, a, ta, bf, af, active );
+    if( active ) { last = 1; it++; active = ((b[4] | b[5] | b[6] | b[7]) != 0u) && it < FD_LAT_MAX_ITER; }
   }
   if( it >= FD_LAT_MAX_ITER ) {
 #pragma unroll
@@ -191,26 +246,36 @@ FD_LT_FN int lat_short_vector( uint32_t const k[ 8 ], uint32_t u[ 8 ], uint32_t 
     *u_neg = 0;
     return it;
   }
-  if( tb[0] & 1u ) {
-    /* (u, v) = (b, (-1)^par tb) */
+  /* (r, tr) = the remainder below 2^128 and its cofactor, (p, tp) = the
+     previous remainder.  Sign: b-side values are +t k, a-side -t k; the
+     cofactor magnitudes tb, ta carry those signs ((-1)^par in the swapped
+     formulation: par = 1 when r sits in a). */
+  uint32_t r[ 8 ], p[ 8 ], tr[ 4 ], tp[ 4 ];
 #pragma unroll
-    for( int j=0; j<8; j++ ) { u[j] = b[j]; v[j] = j < 4 ? tb[j] : 0u; }
+  for( int j=0; j<8; j++ ) { r[j] = last ? b[j] : a[j]; p[j] = last ? a[j] : b[j]; }
+#pragma unroll
+  for( int j=0; j<4; j++ ) { tr[j] = last ? tb[j] : ta[j]; tp[j] = last ? ta[j] : tb[j]; }
+  int par = !last;
+  if( tr[0] & 1u ) {
+    /* (u, v) = (r, (-1)^par tr) */
+#pragma unroll
+    for( int j=0; j<8; j++ ) { u[j] = r[j]; v[j] = j < 4 ? tr[j] : 0u; }
     *u_neg = par;
   } else {
-    /* (u, v) = (a - j b, -(-1)^par (ta + j tb)), j ~ (a - ta) / (b + tb) */
-    double af = lat_f64( a ), bf = lat_f64( b ), taf = lat_f64_4( ta ), tbf = lat_f64_4( tb );
-    double jf = ((af - taf) / (bf + tbf)) * (1.0 - 0x1p-40);
+    /* (u, v) = (p - j r, -(-1)^par (tp + j tr)), j ~ (p - tp) / (r + tr) */
+    double pf = lat_f64( p ), rf = lat_f64( r ), tpf = lat_f64_4( tp ), trf = lat_f64_4( tr );
+    double jf = ((pf - tpf) / (rf + trf)) * (1.0 - 0x1p-40);
     uint32_t jj = jf < 1.0 ? 0u : (jf < 4294967295.0 ? (uint32_t)jf : 0xffffffffu);
-    /* clamp to floor(a/b) (only matters if the estimate is off) */
+    /* clamp to floor(p/r) (only matters if the estimate is off) */
     if( jj ) {
-      int s; uint32_t mq = lat_qest( af, bf, &s );
+      int s; uint32_t mq = lat_qest( pf, rf, &s );
       if( s == 0 && mq < jj ) jj = mq;
     }
-    uint32_t t8[ 8 ] = { ta[0], ta[1], ta[2], ta[3], 0u, 0u, 0u, 0u };
-    uint32_t tb8[ 8 ] = { tb[0], tb[1], tb[2], tb[3], 0u, 0u, 0u, 0u };
-    if( jj ) lat_submul<8>( a, b, t8, tb8, jj, 0 );
+    uint32_t t8[ 8 ] = { tp[0], tp[1], tp[2], tp[3], 0u, 0u, 0u, 0u };
+    uint32_t tr8[ 8 ] = { tr[0], tr[1], tr[2], tr[3], 0u, 0u, 0u, 0u };
+    if( jj ) lat_submul<8>( p, r, t8, tr8, jj, 0 );
 #pragma unroll
-    for( int j=0; j<8; j++ ) { u[j] = a[j]; v[j] = t8[j]; }
+    for( int j=0; j<8; j++ ) { u[j] = p[j]; v[j] = t8[j]; }
     *u_neg = par ^ 1;
   }
   return it;

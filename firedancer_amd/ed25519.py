@@ -30,7 +30,9 @@ class GpuError(RuntimeError):
 
 
 def lib_path():
-    return os.path.join(_HERE, "libfd_ed25519_gpu.so")
+    """The in-tree library; FD_ED25519_GPU_LIB may name a diagnostic build
+    of the same source (tools/Makefile: phase-stamp variant)."""
+    return os.environ.get("FD_ED25519_GPU_LIB") or os.path.join(_HERE, "libfd_ed25519_gpu.so")
 
 
 def load_lib():
@@ -62,6 +64,7 @@ def load_lib():
                                                            ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int)]
     lib.fd_ed25519_gpu_txn_reduce.restype = ctypes.c_int64
     lib.fd_ed25519_gpu_txn_reduce.argtypes = [vp, vp, u64, vp, u64]
+    lib.fd_ed25519_gpu_test_lattice.argtypes = [vp, vp, u64, vp]
     lib.fd_ed25519_gpu_strerror.restype = ctypes.c_char_p
     lib.fd_ed25519_gpu_strerror.argtypes = [i32]
     _LIB = lib
@@ -182,3 +185,13 @@ class Ed25519Gpu:
         if r:
             raise GpuError(strerror(r))
         return out.value
+
+    def test_lattice(self, k_words):
+        """Test hook: device lattice reduction of k (uint32 array [n, 8]) ->
+        uint32 array [n, 18] = |u| (8 words), v (8 words), sign of u, iterations."""
+        k_words = np.ascontiguousarray(k_words, dtype=np.uint32)
+        out = np.zeros((len(k_words), 18), dtype=np.uint32)
+        r = self.lib.fd_ed25519_gpu_test_lattice(self.ctx, _ptr(k_words), len(k_words), _ptr(out))
+        if r:
+            raise GpuError("fd_ed25519_gpu_test_lattice: %s (%d)" % (strerror(r), r))
+        return out

@@ -130,6 +130,12 @@ int64_t fd_ed25519_gpu_txn_reduce( int8_t const * out_code, fd_ed25519_desc_t co
 
 char const * fd_ed25519_gpu_strerror( int err );
 
+/* Test hook (not part of the reference interface): runs the device lattice
+   reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
+   u32 words each, k < l) on the context's first device.  out: n records of
+   18 u32 = |u| (8), v (8), sign of u, iteration count. */
+int fd_ed25519_gpu_test_lattice( fd_ed25519_gpu_t * ctx, uint32_t const * k, uint64_t n, uint32_t * out );
+
 #ifdef __cplusplus
 }
 #endif

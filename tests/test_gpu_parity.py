@@ -153,3 +153,72 @@ def test_bad_descriptor(gpu):
 def test_empty_batch(gpu):
     out = gpu.verify_batch(np.zeros(16, np.uint8), 0, np.zeros(0, fa.DESC_DTYPE))
     assert len(out) == 0
+
+
+L_ORDER = 2**252 + 27742317777372353535851937790883648493
+
+
+def _words_to_int(w):
+    return sum(int(x) << (32 * i) for i, x in enumerate(w))
+
+
+def test_lattice_device_random_and_adversarial_k(gpu):
+    """The device short-vector search (fd_lattice_dev.h) on 200K random k and
+    structured k: u = v k (mod 8l), v odd, 0 < v < l -- the conditions that make
+    [v]([S]B - [k]A - R) == O equivalent to the reference's equation."""
+    rng = np.random.default_rng(5)
+    n = 200_000
+    ks = [int.from_bytes(rng.bytes(32), "little") % L_ORDER for _ in range(n)]
+    ks += [0, 1, 2, 3, L_ORDER - 1, L_ORDER - 2, 2**128 - 1, 2**128, 2**128 + 1, 2**127, 2**200, 2**252,
+           (8 * L_ORDER // 3) % L_ORDER, (8 * L_ORDER // 5) % L_ORDER, 2**64, 12345]
+    ks += [int.from_bytes(rng.bytes(32), "little") % (1 << int(rng.integers(1, 253))) for _ in range(4096)]
+    kw = np.array([[(k >> (32 * j)) & 0xffffffff for j in range(8)] for k in ks], dtype=np.uint32)
+    out = gpu.test_lattice(kw)
+    n8 = 8 * L_ORDER
+    bits = []
+    for i, k in enumerate(ks):
+        u = _words_to_int(out[i, 0:8]) * (-1 if out[i, 16] else 1)
+        v = _words_to_int(out[i, 8:16])
+        assert v % 2 == 1 and 0 < v < L_ORDER, (k, u, v)
+        assert (u - v * k) % n8 == 0, (k, u, v)
+        bits.append(max(abs(u).bit_length(), v.bit_length()))
+    # random k: the vectors are ~2^128 (what the ~130-doubling loop is sized for)
+    assert max(bits[:n]) <= 140 and int(np.percentile(bits[:n], 99)) <= 131
+
+
+def test_fresh_keys_reference_signed(gpu, oracle):
+    """32K distinct keys / messages (so 32K distinct k, R, A), signed here by the
+    reference fd_ed25519_sign (oracle/_ref), variable message lengths 0..1232,
+    a quarter corrupted: codes == the reference fd_ed25519_verify's."""
+    import ctypes, os
+    so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "libfdref_avx512.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle/_ref not built (needs /root/reference in the dev container)")
+    ref = ctypes.CDLL(so)
+    ref.fdref_public_from_private.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    ref.fdref_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
+    ref.fdref_verify.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
+    rng = np.random.default_rng(99)
+    n = 32768
+    recs, exp = [], []
+    for i in range(n):
+        priv = rng.bytes(32)
+        pub = ctypes.create_string_buffer(32); ref.fdref_public_from_private(pub, priv)
+        msg = rng.bytes(int(rng.integers(0, 1233)))
+        sig = ctypes.create_string_buffer(64); ref.fdref_sign(sig, msg, len(msg), pub.raw, priv)
+        s, m = bytearray(sig.raw), bytearray(msg)
+        kind = i & 3
+        if kind == 1 and len(m):
+            m[int(rng.integers(0, len(m)))] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 2:
+            s[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))     # R bit flip
+        elif kind == 3:
+            s[32 + int(rng.integers(0, 31))] ^= 1 << int(rng.integers(0, 8))  # S bit flip
+        recs.append((bytes(m), bytes(s), pub.raw))
+        exp.append(ref.fdref_verify(bytes(m), len(m), bytes(s), pub.raw))
+    arena, desc, sz = fa.pack_batch(recs)
+    out = gpu.verify_batch(arena, sz, desc)
+    exp = np.array(exp, dtype=np.int8)
+    bad = np.nonzero(out != exp)[0]
+    assert len(bad) == 0, [(int(i), int(out[i]), int(exp[i])) for i in bad[:10]]
+    assert np.sum(exp == 0) >= n // 4
