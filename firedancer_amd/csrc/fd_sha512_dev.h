@@ -39,34 +39,61 @@ FD_SHA_CONST uint64_t fd_sha512_dev_K[ 80 ] = {
   0x113f9804bef90daeULL,0x1b710b35131c471bULL,0x28db77f523047d84ULL,0x32caab7b40c72493ULL,0x3c9ebe0a15c9bebcULL,
   0x431d67c49c100d4cULL,0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL };
 
-FD_SHA_FN uint64_t sha_ror( uint64_t x, int n ) { return (x >> n) | (x << (64 - n)); }
+/* 64-bit rotate right by a compile-time n: two v_alignbit_b32 on the
+   32-bit halves (the generic shift/shift/or form costs four 64-bit ops). */
+FD_SHA_FN uint64_t sha_ror( uint64_t x, int n ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if( n >= 32 ) { uint32_t t = lo; lo = hi; hi = t; n -= 32; }
+  if( n == 0 ) return ((uint64_t)hi << 32) | lo;
+  uint32_t rlo = __builtin_amdgcn_alignbit( hi, lo, (uint32_t)n );
+  uint32_t rhi = __builtin_amdgcn_alignbit( lo, hi, (uint32_t)n );
+  return ((uint64_t)rhi << 32) | rlo;
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
+
+/* Ch(e,f,g) = (e & f) ^ (~e & g) = bitfield insert; Maj(a,b,c) = (a^b) ? c : b. */
+FD_SHA_FN uint64_t sha_ch ( uint64_t e, uint64_t f, uint64_t g ) { return (e & f) | (~e & g); }
+FD_SHA_FN uint64_t sha_maj( uint64_t a, uint64_t b, uint64_t c ) { uint64_t m = a ^ b; return (m & c) | (~m & b); }
 
 FD_SHA_FN void sha512_init_state( uint64_t h[ 8 ] ) {
   h[0]=0x6a09e667f3bcc908ULL; h[1]=0xbb67ae8584caa73bULL; h[2]=0x3c6ef372fe94f82bULL; h[3]=0xa54ff53a5f1d36f1ULL;
   h[4]=0x510e527fade682d1ULL; h[5]=0x9b05688c2b3e6c1fULL; h[6]=0x1f83d9abfb41bd6bULL; h[7]=0x5be0cd19137e2179ULL;
 }
 
-/* One 128-byte block, W[16] big-endian words (clobbered). */
+#define SHA_ROUND( a, b, c, d, e, f, g, hh, k, w ) do {                                               \
+    uint64_t t1 = hh + (sha_ror( e, 14 ) ^ sha_ror( e, 18 ) ^ sha_ror( e, 41 )) + sha_ch( e, f, g ) + (k) + (w); \
+    uint64_t t2 = (sha_ror( a, 28 ) ^ sha_ror( a, 34 ) ^ sha_ror( a, 39 )) + sha_maj( a, b, c );           \
+    d += t1; hh = t1 + t2; } while( 0 )
+
+/* One 128-byte block, W[16] big-endian words (clobbered).  16 rounds per
+   loop trip, the eight working variables renamed at compile time (8-round
+   macro groups), the schedule computed in place. */
 FD_SHA_FN void sha512_compress( uint64_t h[ 8 ], uint64_t W[ 16 ] ) {
   uint64_t a=h[0], b=h[1], c=h[2], d=h[3], e=h[4], f=h[5], g=h[6], hh=h[7];
 #pragma unroll 1
   for( int r=0; r<80; r+=16 ) {
+    if( r ) {
 #pragma unroll
-    for( int i=0; i<16; i++ ) {
-      uint64_t w;
-      if( r==0 ) {
-        w = W[i];
-      } else {
+      for( int i=0; i<16; i++ ) {
         uint64_t w15 = W[(i+1)&15], w2 = W[(i+14)&15];
         uint64_t s0 = sha_ror( w15, 1 ) ^ sha_ror( w15, 8 ) ^ (w15 >> 7);
         uint64_t s1 = sha_ror( w2, 19 ) ^ sha_ror( w2, 61 ) ^ (w2 >> 6);
-        w = W[i] + s0 + W[(i+9)&15] + s1;
-        W[i] = w;
+        W[i] = W[i] + s0 + W[(i+9)&15] + s1;
       }
-      uint64_t t1 = hh + (sha_ror( e, 14 ) ^ sha_ror( e, 18 ) ^ sha_ror( e, 41 )) + ((e & f) ^ (~e & g))
-                  + fd_sha512_dev_K[ r+i ] + w;
-      uint64_t t2 = (sha_ror( a, 28 ) ^ sha_ror( a, 34 ) ^ sha_ror( a, 39 )) + ((a & b) ^ (a & c) ^ (b & c));
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+#pragma unroll
+    for( int i=0; i<16; i+=8 ) {
+      SHA_ROUND( a, b, c, d, e, f, g, hh, fd_sha512_dev_K[ r+i   ], W[i  ] );
+      SHA_ROUND( hh, a, b, c, d, e, f, g, fd_sha512_dev_K[ r+i+1 ], W[i+1] );
+      SHA_ROUND( g, hh, a, b, c, d, e, f, fd_sha512_dev_K[ r+i+2 ], W[i+2] );
+      SHA_ROUND( f, g, hh, a, b, c, d, e, fd_sha512_dev_K[ r+i+3 ], W[i+3] );
+      SHA_ROUND( e, f, g, hh, a, b, c, d, fd_sha512_dev_K[ r+i+4 ], W[i+4] );
+      SHA_ROUND( d, e, f, g, hh, a, b, c, fd_sha512_dev_K[ r+i+5 ], W[i+5] );
+      SHA_ROUND( c, d, e, f, g, hh, a, b, fd_sha512_dev_K[ r+i+6 ], W[i+6] );
+      SHA_ROUND( b, c, d, e, f, g, hh, a, fd_sha512_dev_K[ r+i+7 ], W[i+7] );
     }
   }
   h[0]+=a; h[1]+=b; h[2]+=c; h[3]+=d; h[4]+=e; h[5]+=f; h[6]+=g; h[7]+=hh;
