@@ -9,9 +9,9 @@ verify hot path (fd_ed25519_verify_batch_gpu_dev) over that batch.  With
 own 64K batch: weak scaling, no collective on the data path (signatures are
 independent; the barrier + MAX-over-ranks timing is the only exchange).
 
-Synthetic data: the 1,024 config-1 signatures (distinct keys, 200-byte random
-messages, signed by the reference fd_ed25519_sign, tests/golden/synthetic.bin
-set 10), tiled to 65,536 descriptors, each with its own copy in the arena.
+Synthetic data: 65,536 distinct keys and 200-byte random messages per rank
+(fixed seed), signed on the host by the reference fd_ed25519_sign compiled
+from the reference sources (oracle/_ref), one arena record per signature.
 
 Extra keys beside the contract fields:
   roofline     -- INT32 VALU multiply-add roofline of the verify kernel
@@ -19,7 +19,7 @@ Extra keys beside the contract fields:
                   / mean launch time (HIP events on the launch stream),
                   peak = measured v_mad_u64_u32 rate (profiles/r01/valu_probe.json)
                   x 256 CU x 2.4 GHz; traffic = HBM bytes per launch from a
-                  rocprofv3 PMC pass (profiles/r01/pmc_traffic.json) or null.
+                  rocprofv3 PMC pass (profiles/r01/pmc_traffic.json, gfx950 FETCH_SIZE x2 correction) or null.
   cpu_baseline -- the reference fd_ed25519_verify (AVX-512 build when the host
                   has avx512ifma, else the portable build) compiled from the
                   reference sources (oracle/_ref), on a bounded sample of the
@@ -45,17 +45,61 @@ NOMINAL_GHZ = 2.4
 N_CU = 256
 
 
+def _ref_signer():
+    """The reference fd_ed25519_sign / public_from_private (oracle/_ref, built
+    from the reference sources in the dev container; test/bench infrastructure)."""
+    path = os.path.join(REPO, "oracle", "_ref", "libfdref_avx512.so")
+    if not os.path.exists(path):
+        path = os.path.join(REPO, "oracle", "_ref", "libfdref_ref.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.fdref_public_from_private.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    lib.fdref_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
+    return lib
+
+
 def build_workload(n, msg_sz, seed):
+    """n DISTINCT reference-signed signatures (fresh key + msg_sz random bytes each,
+    fixed seed), signed on the host by the reference fd_ed25519_sign in 16 threads.
+    Falls back to tiling the 1024 committed config-1 signatures only if the
+    reference library is missing."""
     import firedancer_amd as fa
-    from golden_io import read_sigs
-    base = [r for r in read_sigs("synthetic.bin") if r["set"] == 10]
-    assert len(base) == 1024 and all(len(r["msg"]) == 200 for r in base)
-    if msg_sz != 200:
-        raise SystemExit("only the 200-byte config-2 workload is tiled from reference-signed inputs")
-    rot = seed % len(base)
-    recs = [(base[(i + rot) % 1024]["msg"], base[(i + rot) % 1024]["sig"], base[(i + rot) % 1024]["pub"])
-            for i in range(n)]
-    return fa.pack_batch(recs)
+    ref = _ref_signer()
+    if ref is None:
+        from golden_io import read_sigs
+        base = [r for r in read_sigs("synthetic.bin") if r["set"] == 10]
+        if msg_sz != 200:
+            raise SystemExit("reference signer missing: only the 200-byte tiled workload is available")
+        rot = seed % len(base)
+        recs = [(base[(i + rot) % 1024]["msg"], base[(i + rot) % 1024]["sig"], base[(i + rot) % 1024]["pub"])
+                for i in range(n)]
+        arena, desc, sz = fa.pack_batch(recs)
+        return arena, desc, sz, "1024 reference-signed config-1 signatures tiled to %d descriptors" % n
+    rng = np.random.default_rng(1234 + seed)
+    privs = rng.bytes(32 * n)
+    msgs = rng.bytes(msg_sz * n)
+    pubs = [None] * n
+    sigs = [None] * n
+
+    def work(lo, hi):
+        for i in range(lo, hi):
+            priv = privs[32 * i:32 * i + 32]
+            msg = msgs[msg_sz * i:msg_sz * i + msg_sz]
+            pub = ctypes.create_string_buffer(32)
+            ref.fdref_public_from_private(pub, priv)
+            sig = ctypes.create_string_buffer(64)
+            ref.fdref_sign(sig, msg, msg_sz, pub.raw, priv)
+            pubs[i] = pub.raw
+            sigs[i] = sig.raw
+    from concurrent.futures import ThreadPoolExecutor
+    nt = 16
+    with ThreadPoolExecutor(nt) as ex:
+        list(ex.map(lambda t: work(n * t // nt, n * (t + 1) // nt), range(nt)))
+    recs = [(msgs[msg_sz * i:msg_sz * i + msg_sz], sigs[i], pubs[i]) for i in range(n)]
+    arena, desc, sz = fa.pack_batch(recs)
+    return arena, desc, sz, "%d distinct keys and %d-B random messages (seed %d), signed by the reference " \
+                            "fd_ed25519_sign (oracle/_ref), all valid" % (n, msg_sz, 1234 + seed)
 
 
 def valu_peak():
@@ -132,7 +176,7 @@ def main():
     dev = torch.device("cuda", local)
 
     n = args.batch
-    arena, desc, sz = build_workload(n, args.msg_sz, seed=rank)
+    arena, desc, sz, data_desc = build_workload(n, args.msg_sz, seed=rank)
     g = fa.Ed25519Gpu(device_mask=1 << local, max_batch=n)
     d_arena = torch.from_numpy(arena).to(dev)
     d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
@@ -184,8 +228,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic: 1024 reference-signed config-1 signatures (distinct keys, 200-B messages) "
-                    "tiled to %d descriptors per GPU, all valid" % n,
+            "data": "synthetic: " + data_desc,
             "config": {"workload": "config2: %d-signature batch per GPU, fixed %d-B messages, device-resident"
                                    % (n, args.msg_sz),
                        "batch_per_gpu": n, "msg_sz": args.msg_sz, "parallelism": "shard-per-gpu x%d" % world},

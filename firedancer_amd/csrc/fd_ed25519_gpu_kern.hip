@@ -1,52 +1,26 @@
-/* fd_ed25519_gpu.hip -- MI355X (gfx950) Ed25519 batch verifier: kernels and
-   the C ABI declared in include/fd_ed25519_gpu.h.
+/* fd_ed25519_gpu_kern.hip -- MI355X (gfx950) Ed25519 batch verifier: the
+   device code.  Built to gfx950 assembly, passed through the peephole
+   rewriter tools/asm_peephole.py, assembled into a code object that the host
+   runtime (fd_ed25519_gpu_host.cpp) embeds, loads and launches by name.
 
-   One signature per lane.  The verify kernel does, per lane:
-     S < l check -> decode A, R (sqrt-ratio ladder) -> small-order checks ->
-     SHA-512(R || A || M) with M streamed from HBM -> reduce mod l ->
-     signed fixed-window recoding of k (4-bit) and S (8-bit) ->
-     table of [0..8](-A) in a per-lane HBM/L2 scratch -> joint double-scalar
-     multiplication [k](-A) + [S]B with the [0..128]B affine table in LDS ->
-     projective compare against R.
+   One signature per lane:
+     S < l check -> k = SHA-512(R || A || M) mod l (M streamed from HBM) ->
+     short vector (u, v) of the lattice {u = v k mod 8l}, w = v S mod l
+     (fd_lattice_dev.h) -> decode A and R (sqrt-ratio ladder), small-order
+     checks -> per-lane tables [0..8](-A), [0..8](-R) in HBM ->
+     Q = [u](-A) + [v](-R) + [w]B in ONE ~130-doubling Straus chain, the B
+     part from the LDS tables of [0..128]B and [0..128]2^128 B -> Q == O.
    Semantics follow fd_ed25519_verify (src/ballet/ed25519/fd_ed25519_user.c:
-   134-229) with the FD_HAS_AVX512 error mapping (SURVEY.md §8(a) A-spec).
-
-   Host side: a context owns, per device, a stream, the B table, descriptor /
-   arena / code staging buffers and the A-table scratch.  Batches are sharded
-   contiguously over the context's devices; no collective is needed (every
-   signature is independent). */
+   134-229) with the FD_HAS_AVX512 error mapping (SURVEY.md §8(a) A-spec). */
 
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
-#include <string.h>
-#include <stdio.h>
 
-#include "../../include/fd_ed25519_gpu.h"
+#include "fd_ed25519_gpu_abi.h"
 #include "fd_f25519_dev.h"
 #include "fd_curve25519_dev.h"
 #include "fd_sha512_dev.h"
 #include "fd_scalar_dev.h"
 #include "fd_lattice_dev.h"
-
-#define FD_VERIFY_BLOCK   256          /* threads per workgroup: 4 waves              */
-#ifndef FD_VERIFY_WAVES_PER_EU
-#define FD_VERIFY_WAVES_PER_EU 2       /* -> <= 256 VGPR+AGPR per lane                */
-#endif
-#define FD_BTAB_N         129          /* [0..128]P                                   */
-#define FD_BTAB_STRIDE    32           /* u32 per entry: 3 x 10 limbs + pad           */
-#define FD_BTAB_WORDS     (2 * FD_BTAB_N * FD_BTAB_STRIDE)   /* P = B and P = 2^128 B */
-#define FD_BTAB_LOADS     ((FD_BTAB_WORDS/4 + FD_VERIFY_BLOCK - 1) / FD_VERIFY_BLOCK)   /* uint4 per thread */
-#define FD_BTAB_ALLOC     (FD_BTAB_LOADS * FD_VERIFY_BLOCK * 4)                       /* padded u32 */
-#define FD_VTAB_N         9            /* [0..8](-Q), Q = A or R                      */
-#define FD_VTAB_WORDS     40           /* u32 per entry (4 fe)                        */
-#define FD_NDIG_MAX       64           /* 4-bit windows of a <= 256-bit scalar        */
-
-/* LDS digit rows ([row][slot] bytes) */
-#define FD_ROW_U          0            /* signed 4-bit digits of u (sign folded in)   */
-#define FD_ROW_V          64           /* signed 4-bit digits of v                    */
-#define FD_ROW_W          128          /* signed 8-bit digits of w = v S mod l (32)   */
-#define FD_ROW_NW         160          /* lane 0 of each wave: the wave's window count */
-#define FD_ROWS           161
 
 /* Diagnostic build only (-DFD_PHASE_STAMPS, tools/Makefile): s_memtime at
    phase boundaries, per-wave deltas summed into args.stamps.  The product
@@ -90,7 +64,7 @@ __device__ void ge_affine_precomp( ge_precomp & q, ge_p3 & p ) {
    stores its affine precomputed form (Y+X, Y-X, 2dXY) at
    btab[(t*FD_BTAB_N + i)*FD_BTAB_STRIDE ...].  B decoded from its standard
    encoding (y = 4/5, x even). */
-__global__ void fd_ed25519_btab_init( uint32_t * btab ) {
+extern "C" __global__ void fd_ed25519_btab_init( uint32_t * btab ) {
   int g = blockIdx.x * blockDim.x + threadIdx.x;
   if( g >= 2*FD_BTAB_N ) return;
   int t = g / FD_BTAB_N, i = g % FD_BTAB_N;
@@ -116,18 +90,7 @@ __global__ void fd_ed25519_btab_init( uint32_t * btab ) {
 
 /* ------------------------------------------------------------------ verify */
 
-struct verify_args {
-  uint8_t const *           arena;
-  uint64_t                  arena_sz;
-  fd_ed25519_desc_t const * desc;
-  uint64_t                  n;
-  int8_t *                  out;
-  uint32_t const *          btab;      /* FD_BTAB_WORDS u32                        */
-  uint32_t *                vtab;      /* FD_VTAB_N * FD_VTAB_WORDS * vtab_cap u32 */
-  uint64_t                  vtab_cap;  /* tables                                   */
-  int                       ref_codes;
-  unsigned long long *      stamps;    /* FD_PHASE_STAMPS builds only: per-phase cycle sums */
-};
+/* struct verify_args: fd_ed25519_gpu_abi.h */
 
 /* Raw message dwords of SHA block b: dword (msg_off>>2) + 32b - 16 + i,
    i < 33, clamped to the readable arena (block 0's first 16 are unused:
@@ -354,7 +317,7 @@ __device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 
    (Q = [v]([S]B - [k]A - R), fd_lattice_dev.h).  The reported code follows
    the reference's check order (fd_ed25519_user.c:157-228): S, decode A,
    decode R, small-order A, small-order R, equation. */
-__global__ void __launch_bounds__( FD_VERIFY_BLOCK, FD_VERIFY_WAVES_PER_EU )
+extern "C" __global__ void __launch_bounds__( FD_VERIFY_BLOCK, FD_VERIFY_WAVES_PER_EU )
 fd_ed25519_verify_kernel( verify_args args ) {
   __shared__ uint4    s_btab4[ FD_BTAB_WORDS / 4 ];
   __shared__ uint8_t  s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
@@ -507,7 +470,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
 
 /* Self-test kernel (tests only, fd_ed25519_gpu_test_lattice): the device
    lattice reduction on caller-supplied k, one per lane. */
-__global__ void fd_ed25519_lattice_test_kernel( uint32_t const * k, uint32_t * out, uint64_t n ) {
+extern "C" __global__ void fd_ed25519_lattice_test_kernel( uint32_t const * k, uint32_t * out, uint64_t n ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t kk[ 8 ], u[ 8 ], v[ 8 ];
   int un = 0, it = 0;
@@ -522,341 +485,3 @@ __global__ void fd_ed25519_lattice_test_kernel( uint32_t const * k, uint32_t * o
   }
 }
 
-/* ------------------------------------------------------------------ host side */
-
-#define FD_MAX_DEV 16
-
-struct fd_dev_state {
-  int          dev;
-  hipStream_t  stream;
-  hipEvent_t   done;
-  uint32_t *   btab;        /* device */
-  uint32_t *   vtab;        /* device, FD_VTAB_N*FD_VTAB_WORDS*vtab_cap u32 */
-  uint64_t     vtab_cap;    /* tables (2 per signature) */
-  uint64_t     sig_cap;     /* signatures per launch     */
-  unsigned long long * stamps; /* FD_PHASE_STAMPS builds only */
-  uint8_t *    d_arena;  uint64_t arena_cap;
-  fd_ed25519_desc_t * d_desc; uint64_t desc_cap;
-  int8_t *     d_out;
-  int          busy;
-};
-
-struct fd_ed25519_gpu {
-  int          ndev;
-  uint64_t     max_batch;
-  int          ref_codes;
-  fd_dev_state d[ FD_MAX_DEV ];
-  /* pending async batch */
-  int8_t *     pend_out;
-  uint64_t     pend_cnt;
-  int          pend_active;
-};
-
-#define HIPCK( x ) do { hipError_t _e = (x); if( _e != hipSuccess ) { \
-    fprintf( stderr, "fd_ed25519_gpu: %s failed: %s (%s:%d)\n", #x, hipGetErrorString( _e ), __FILE__, __LINE__ ); \
-    return FD_ED25519_GPU_ERR_LAUNCH; } } while( 0 )
-
-static uint64_t align_up( uint64_t x, uint64_t a ) { return (x + a - 1u) / a * a; }
-
-static int dev_reserve( fd_dev_state * s, uint64_t arena_sz, uint64_t cnt ) {
-  HIPCK( hipSetDevice( s->dev ) );
-  uint64_t need_arena = align_up( arena_sz, 4u ) + 16u;
-  if( need_arena > s->arena_cap ) {
-    if( s->d_arena ) HIPCK( hipFree( s->d_arena ) );
-    s->arena_cap = align_up( need_arena * 5u / 4u, 1u << 20 );
-    if( hipMalloc( &s->d_arena, s->arena_cap ) != hipSuccess ) { s->d_arena = NULL; s->arena_cap = 0; return FD_ED25519_GPU_ERR_OOM; }
-  }
-  if( cnt > s->desc_cap ) {
-    if( s->d_desc ) HIPCK( hipFree( s->d_desc ) );
-    if( s->d_out )  HIPCK( hipFree( s->d_out ) );
-    s->desc_cap = align_up( cnt, 4096u );
-    if( hipMalloc( &s->d_desc, s->desc_cap * sizeof(fd_ed25519_desc_t) ) != hipSuccess ||
-        hipMalloc( &s->d_out, s->desc_cap ) != hipSuccess ) { s->desc_cap = 0; return FD_ED25519_GPU_ERR_OOM; }
-  }
-  return FD_ED25519_GPU_OK;
-}
-
-/* Enqueue kernels over [0, cnt) of device-resident descriptors, chunked to
-   the A-table scratch capacity. */
-static int dev_launch( fd_ed25519_gpu_t * ctx, fd_dev_state * s, uint8_t const * d_arena, uint64_t arena_sz,
-                       fd_ed25519_desc_t const * d_desc, uint64_t cnt, int8_t * d_out, hipStream_t st ) {
-  HIPCK( hipSetDevice( s->dev ) );
-  for( uint64_t off=0; off<cnt; off+=s->sig_cap ) {
-    uint64_t m = cnt - off < s->sig_cap ? cnt - off : s->sig_cap;
-    verify_args a;
-    a.arena = d_arena; a.arena_sz = arena_sz; a.desc = d_desc + off; a.n = m; a.out = d_out + off;
-    a.btab = s->btab; a.vtab = s->vtab; a.vtab_cap = s->vtab_cap; a.ref_codes = ctx->ref_codes;
-    a.stamps = s->stamps;
-    uint32_t blocks = (uint32_t)((m + FD_VERIFY_BLOCK - 1u) / FD_VERIFY_BLOCK);
-    hipLaunchKernelGGL( fd_ed25519_verify_kernel, dim3( blocks ), dim3( FD_VERIFY_BLOCK ), 0, st, a );
-    HIPCK( hipGetLastError() );
-  }
-  return FD_ED25519_GPU_OK;
-}
-
-extern "C" {
-
-fd_ed25519_gpu_t *
-fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch ) {
-  int cnt = 0;
-  if( hipGetDeviceCount( &cnt ) != hipSuccess || cnt <= 0 ) return NULL;
-  fd_ed25519_gpu_t * ctx = (fd_ed25519_gpu_t *)calloc( 1, sizeof(fd_ed25519_gpu_t) );
-  if( !ctx ) return NULL;
-  if( !max_batch ) max_batch = 1u << 18;
-  ctx->max_batch = max_batch;
-  if( !device_mask ) { int cur = 0; hipGetDevice( &cur ); device_mask = 1ull << cur; }
-  for( int i=0; i<cnt && i<FD_MAX_DEV; i++ ) {
-    if( !((device_mask >> i) & 1u) ) continue;
-    fd_dev_state * s = &ctx->d[ ctx->ndev ];
-    s->dev = i;
-    if( hipSetDevice( i ) != hipSuccess ) goto fail;
-    if( hipStreamCreateWithFlags( &s->stream, hipStreamNonBlocking ) != hipSuccess ) goto fail;
-    if( hipEventCreateWithFlags( &s->done, hipEventDisableTiming ) != hipSuccess ) goto fail;
-    if( hipMalloc( &s->btab, FD_BTAB_ALLOC * sizeof(uint32_t) ) != hipSuccess ) goto fail;
-    if( hipMemsetAsync( s->btab, 0, FD_BTAB_ALLOC * sizeof(uint32_t), s->stream ) != hipSuccess ) goto fail;
-    s->sig_cap  = align_up( max_batch, FD_VERIFY_BLOCK );
-    s->vtab_cap = 2u * s->sig_cap;   /* tables of -A at [0, sig_cap), of -R at [sig_cap, 2 sig_cap) */
-    if( hipMalloc( &s->vtab, (uint64_t)FD_VTAB_N * FD_VTAB_WORDS * s->vtab_cap * sizeof(uint32_t) ) != hipSuccess ) goto fail;
-#ifdef FD_PHASE_STAMPS
-    if( hipMalloc( &s->stamps, 8 * sizeof(unsigned long long) ) != hipSuccess ) goto fail;
-    hipMemset( s->stamps, 0, 8 * sizeof(unsigned long long) );
-#endif
-    ctx->ndev++;
-    hipLaunchKernelGGL( fd_ed25519_btab_init, dim3( (2*FD_BTAB_N + 63)/64 ), dim3( 64 ), 0, s->stream, s->btab );
-    if( hipStreamSynchronize( s->stream ) != hipSuccess ) goto fail;
-  }
-  if( !ctx->ndev ) goto fail;
-  return ctx;
-fail:
-  fd_ed25519_gpu_delete( ctx );
-  return NULL;
-}
-
-void
-fd_ed25519_gpu_delete( fd_ed25519_gpu_t * ctx ) {
-  if( !ctx ) return;
-  for( int i=0; i<FD_MAX_DEV; i++ ) {
-    fd_dev_state * s = &ctx->d[i];
-    if( !s->stream && !s->btab ) continue;
-    hipSetDevice( s->dev );
-    if( s->stream ) hipStreamSynchronize( s->stream );
-    if( s->btab )    hipFree( s->btab );
-    if( s->vtab )    hipFree( s->vtab );
-#ifdef FD_PHASE_STAMPS
-    if( s->stamps ) {
-      unsigned long long h[ 8 ];
-      if( hipMemcpy( h, s->stamps, sizeof(h), hipMemcpyDeviceToHost ) == hipSuccess && h[7] ) {
-        char const * nm[ 6 ] = { "prologue", "sha", "lattice", "decode+tab", "loop", "tail" };
-        unsigned long long tot = 0; for( int i=0; i<6; i++ ) tot += h[i];
-        for( int i=0; i<6; i++ ) fprintf( stderr, "stamp %-10s %12.0f cyc/wave  %5.1f%%\n", nm[i], (double)h[i]/(double)h[7], 100.0*(double)h[i]/(double)tot );
-      }
-      hipFree( s->stamps );
-    }
-#endif
-    if( s->d_arena ) hipFree( s->d_arena );
-    if( s->d_desc )  hipFree( s->d_desc );
-    if( s->d_out )   hipFree( s->d_out );
-    if( s->done )    hipEventDestroy( s->done );
-    if( s->stream )  hipStreamDestroy( s->stream );
-  }
-  free( ctx );
-}
-
-int fd_ed25519_gpu_device_cnt( fd_ed25519_gpu_t const * ctx ) { return ctx ? ctx->ndev : 0; }
-
-int
-fd_ed25519_gpu_set_codes( fd_ed25519_gpu_t * ctx, int flavour ) {
-  if( !ctx || (flavour != FD_ED25519_GPU_CODES_AVX512 && flavour != FD_ED25519_GPU_CODES_REF) ) return FD_ED25519_GPU_ERR_ARG;
-  ctx->ref_codes = flavour;
-  return FD_ED25519_GPU_OK;
-}
-
-static int
-check_descs( uint64_t arena_sz, fd_ed25519_desc_t const * desc, uint64_t n ) {
-  for( uint64_t i=0; i<n; i++ ) {
-    fd_ed25519_desc_t const * d = desc + i;
-    if( (uint64_t)d->sig_off + 64u > arena_sz || (uint64_t)d->pub_off + 32u > arena_sz ||
-        (uint64_t)d->msg_off + d->msg_sz > arena_sz ) return FD_ED25519_GPU_ERR_ARG;
-  }
-  return FD_ED25519_GPU_OK;
-}
-
-int
-fd_ed25519_gpu_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
-                       fd_ed25519_desc_t const * desc, uint64_t desc_cnt, int8_t * out_code ) {
-  if( !ctx ) return FD_ED25519_GPU_ERR_ARG;
-  if( ctx->pend_active ) return FD_ED25519_GPU_ERR_BUSY;
-  if( desc_cnt && (!arena || !desc || !out_code) ) return FD_ED25519_GPU_ERR_ARG;
-  if( arena_sz > 0xffffffffull + 1ull ) return FD_ED25519_GPU_ERR_ARG;
-  int err = check_descs( arena_sz, desc, desc_cnt );
-  if( err ) return err;
-  ctx->pend_out = out_code; ctx->pend_cnt = desc_cnt; ctx->pend_active = 1;
-  for( int i=0; i<ctx->ndev; i++ ) {
-    fd_dev_state * s = &ctx->d[i];
-    uint64_t lo = desc_cnt * (uint64_t)i / (uint64_t)ctx->ndev;
-    uint64_t hi = desc_cnt * (uint64_t)(i+1) / (uint64_t)ctx->ndev;
-    uint64_t m = hi - lo;
-    s->busy = 0;
-    if( !m ) continue;
-    if( (err = dev_reserve( s, arena_sz, m )) ) { ctx->pend_active = 0; return err; }
-    /* Each device gets the whole arena (descriptors index it freely). */
-    HIPCK( hipMemcpyAsync( s->d_arena, arena, arena_sz, hipMemcpyHostToDevice, s->stream ) );
-    HIPCK( hipMemcpyAsync( s->d_desc, desc + lo, m * sizeof(fd_ed25519_desc_t), hipMemcpyHostToDevice, s->stream ) );
-    if( (err = dev_launch( ctx, s, s->d_arena, arena_sz, s->d_desc, m, s->d_out, s->stream )) ) { ctx->pend_active = 0; return err; }
-    HIPCK( hipMemcpyAsync( out_code + lo, s->d_out, m, hipMemcpyDeviceToHost, s->stream ) );
-    HIPCK( hipEventRecord( s->done, s->stream ) );
-    s->busy = 1;
-  }
-  return FD_ED25519_GPU_OK;
-}
-
-int
-fd_ed25519_gpu_poll( fd_ed25519_gpu_t * ctx ) {
-  if( !ctx ) return FD_ED25519_GPU_ERR_ARG;
-  if( !ctx->pend_active ) return FD_ED25519_GPU_OK;
-  for( int i=0; i<ctx->ndev; i++ ) {
-    fd_dev_state * s = &ctx->d[i];
-    if( !s->busy ) continue;
-    hipSetDevice( s->dev );
-    hipError_t e = hipEventQuery( s->done );
-    if( e == hipErrorNotReady ) return FD_ED25519_GPU_PENDING;
-    if( e != hipSuccess ) { ctx->pend_active = 0; return FD_ED25519_GPU_ERR_LAUNCH; }
-    s->busy = 0;
-  }
-  ctx->pend_active = 0;
-  return FD_ED25519_GPU_OK;
-}
-
-int
-fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
-                             fd_ed25519_desc_t const * desc, uint64_t desc_cnt, int8_t * out_code ) {
-  int err = fd_ed25519_gpu_submit( ctx, arena, arena_sz, desc, desc_cnt, out_code );
-  if( err ) return err;
-  for( int i=0; i<ctx->ndev; i++ ) {
-    fd_dev_state * s = &ctx->d[i];
-    if( !s->busy ) continue;
-    hipSetDevice( s->dev );
-    if( hipEventSynchronize( s->done ) != hipSuccess ) { ctx->pend_active = 0; return FD_ED25519_GPU_ERR_LAUNCH; }
-  }
-  return fd_ed25519_gpu_poll( ctx );
-}
-
-int
-fd_ed25519_verify_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx, uint8_t const * d_arena, uint64_t arena_sz,
-                                 fd_ed25519_desc_t const * d_desc, uint64_t desc_cnt, int8_t * d_out, void * stream ) {
-  if( !ctx || dev_idx < 0 || dev_idx >= ctx->ndev ) return FD_ED25519_GPU_ERR_ARG;
-  if( !desc_cnt ) return FD_ED25519_GPU_OK;
-  if( !d_arena || !d_desc || !d_out ) return FD_ED25519_GPU_ERR_ARG;
-  fd_dev_state * s = &ctx->d[ dev_idx ];
-  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-  return dev_launch( ctx, s, d_arena, arena_sz, d_desc, desc_cnt, d_out, st );
-}
-
-int
-fd_ed25519_gpu_verify( fd_ed25519_gpu_t * ctx, uint8_t const * msg, uint64_t msg_sz,
-                       uint8_t const sig[ 64 ], uint8_t const pub[ 32 ], int * out ) {
-  if( !ctx || !out || !sig || !pub || (msg_sz && !msg) || msg_sz > 0xffffu ) return FD_ED25519_GPU_ERR_ARG;
-  uint64_t sz = 96u + msg_sz;
-  uint8_t * arena = (uint8_t *)malloc( sz + 16u );
-  if( !arena ) return FD_ED25519_GPU_ERR_OOM;
-  memcpy( arena, sig, 64 ); memcpy( arena + 64, pub, 32 ); if( msg_sz ) memcpy( arena + 96, msg, msg_sz );
-  fd_ed25519_desc_t d = { 0u, 64u, 96u, (uint16_t)msg_sz, 0u };
-  int8_t code = 0;
-  int err = fd_ed25519_verify_batch_gpu( ctx, arena, sz, &d, 1u, &code );
-  free( arena );
-  if( err ) return err;
-  *out = code;
-  return FD_ED25519_GPU_OK;
-}
-
-int
-fd_ed25519_gpu_verify_batch_single_msg( fd_ed25519_gpu_t * ctx, uint8_t const * msg, uint64_t msg_sz,
-                                        uint8_t const * sigs, uint8_t const * pubs, uint64_t n, int * out ) {
-  if( !ctx || !out || (msg_sz && !msg) || msg_sz > 0xffffu ) return FD_ED25519_GPU_ERR_ARG;
-  if( n == 0u || n > 16u ) { *out = FD_ED25519_ERR_SIG; return FD_ED25519_GPU_OK; }   /* fd_ed25519_user.c:238-240 */
-  if( !sigs || !pubs ) return FD_ED25519_GPU_ERR_ARG;
-  uint64_t sz = 96u * n + msg_sz;
-  uint8_t * arena = (uint8_t *)malloc( sz + 16u );
-  if( !arena ) return FD_ED25519_GPU_ERR_OOM;
-  memcpy( arena, sigs, 64u * n ); memcpy( arena + 64u * n, pubs, 32u * n );
-  if( msg_sz ) memcpy( arena + 96u * n, msg, msg_sz );
-  fd_ed25519_desc_t d[ 16 ];
-  for( uint64_t j=0; j<n; j++ ) {
-    d[j].sig_off = (uint32_t)(64u * j); d[j].pub_off = (uint32_t)(64u * n + 32u * j);
-    d[j].msg_off = (uint32_t)(96u * n); d[j].msg_sz = (uint16_t)msg_sz; d[j].txn_idx = 0u;
-  }
-  int8_t codes[ 16 ];
-  int err = fd_ed25519_verify_batch_gpu( ctx, arena, sz, d, n, codes );
-  free( arena );
-  if( err ) return err;
-  int8_t t;
-  fd_ed25519_gpu_txn_reduce( codes, d, n, &t, 1u );
-  *out = t;
-  return FD_ED25519_GPU_OK;
-}
-
-int64_t
-fd_ed25519_gpu_txn_reduce( int8_t const * out_code, fd_ed25519_desc_t const * desc, uint64_t n,
-                           int8_t * out_txn_code, uint64_t out_cap ) {
-  int64_t t = 0;
-  uint64_t i = 0;
-  while( i < n ) {
-    uint64_t j = i;
-    while( j < n && desc[j].txn_idx == desc[i].txn_idx ) j++;
-    int8_t code = FD_ED25519_SUCCESS;
-    if( j - i > 16u ) code = FD_ED25519_ERR_SIG;
-    else {
-      int8_t first_p1 = 0, any_msg = 0;
-      for( uint64_t k=i; k<j; k++ ) {
-        int8_t c = out_code[k];
-        if( c == FD_ED25519_ERR_MSG ) any_msg = 1;
-        else if( c != FD_ED25519_SUCCESS && !first_p1 ) first_p1 = c;
-      }
-      code = first_p1 ? first_p1 : (any_msg ? (int8_t)FD_ED25519_ERR_MSG : (int8_t)FD_ED25519_SUCCESS);
-    }
-    if( (uint64_t)t < out_cap ) out_txn_code[t] = code;
-    t++;
-    i = j;
-  }
-  return t;
-}
-
-int
-fd_ed25519_gpu_test_lattice( fd_ed25519_gpu_t * ctx, uint32_t const * k, uint64_t n, uint32_t * out ) {
-  if( !ctx || !k || !out || !n ) return FD_ED25519_GPU_ERR_ARG;
-  fd_dev_state * s = &ctx->d[0];
-  HIPCK( hipSetDevice( s->dev ) );
-  uint32_t * dk = NULL; uint32_t * dout = NULL;
-  HIPCK( hipMalloc( &dk, n * 32u ) );
-  if( hipMalloc( &dout, n * 72u ) != hipSuccess ) { hipFree( dk ); return FD_ED25519_GPU_ERR_OOM; }
-  int err = FD_ED25519_GPU_OK;
-  if( hipMemcpy( dk, k, n * 32u, hipMemcpyHostToDevice ) != hipSuccess ) err = FD_ED25519_GPU_ERR_LAUNCH;
-  if( !err ) {
-    hipLaunchKernelGGL( fd_ed25519_lattice_test_kernel, dim3( (uint32_t)((n + 255u) / 256u) ), dim3( 256 ), 0, s->stream, dk, dout, n );
-    if( hipGetLastError() != hipSuccess || hipStreamSynchronize( s->stream ) != hipSuccess ) err = FD_ED25519_GPU_ERR_LAUNCH;
-  }
-  if( !err && hipMemcpy( out, dout, n * 72u, hipMemcpyDeviceToHost ) != hipSuccess ) err = FD_ED25519_GPU_ERR_LAUNCH;
-  hipFree( dk ); hipFree( dout );
-  return err;
-}
-
-char const *
-fd_ed25519_gpu_strerror( int err ) {
-  switch( err ) {
-  case FD_ED25519_SUCCESS:         return "success";
-  case FD_ED25519_ERR_SIG:         return "bad signature";
-  case FD_ED25519_ERR_PUBKEY:      return "bad public key";
-  case FD_ED25519_ERR_MSG:         return "bad message";
-  case FD_ED25519_GPU_PENDING:     return "pending";
-  case FD_ED25519_GPU_ERR_NODEV:   return "no gpu device";
-  case FD_ED25519_GPU_ERR_OOM:     return "gpu out of memory";
-  case FD_ED25519_GPU_ERR_LAUNCH:  return "gpu launch/runtime failure";
-  case FD_ED25519_GPU_ERR_ARG:     return "bad argument";
-  case FD_ED25519_GPU_ERR_BUSY:    return "batch already in flight";
-  case FD_ED25519_GPU_CODE_BAD_DESC: return "descriptor outside arena";
-  default: break;
-  }
-  return "unknown";
-}
-
-} /* extern "C" */

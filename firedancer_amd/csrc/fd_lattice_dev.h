@@ -180,27 +180,106 @@ FD_LT_FN double lat_rcp( double y ) {
 /* a < b, 8 words */
 FD_LT_FN int lat_lt( uint32_t const a[ 8 ], uint32_t const b[ 8 ] ) { return !lat_ge( a, b ); }
 
-/* One Euclid half-step on (x, tx) by (y, ty), y >= 2^128, x > y on entry:
-   x -= m y, tx += m ty with m the f64 quotient estimate (1 <= m <=
-   floor(x/y)), repeated (rarely) until x < y.  xf/yf: f64 approximations
-   of x/y on entry; xf is refreshed on exit. */
-FD_LT_FN void lat_reduce( uint32_t x[ 8 ], uint32_t tx[ 4 ], uint32_t const y[ 8 ], uint32_t const ty[ 4 ],
-                          double & xf, double yf, int act ) {
-  double ry = lat_rcp( yf );
-  double q = (xf * ry) * (1.0 - 0x1p-40);
-  int big = act && q >= 4294967296.0;
-  if( lat_any( big ) ) {
-    if( big ) {                                   /* rare: quotient >= 2^32 */
-      int s; uint32_t m = lat_qest( lat_f64( x ), lat_f64( y ), &s );
-      lat_submul<4>( x, y, tx, ty, m, s );
+/* 8-word x: word i selected by a lane-varying i in [2, 7] (select chain, no
+   dynamic register indexing). */
+FD_LT_FN uint32_t lat_word( uint32_t const x[ 8 ], int i ) {
+  uint32_t r = x[2];
+  r = i == 3 ? x[3] : r; r = i == 4 ? x[4] : r; r = i == 5 ? x[5] : r;
+  r = i == 6 ? x[6] : r; r = i == 7 ? x[7] : r;
+  return r;
+}
+
+/* r = m x - n y (9-word two's complement, the caller knows the sign), m, n < 2^32 */
+FD_LT_FN void lat_mxny( uint32_t r[ 9 ], uint32_t m, uint32_t const x[ 8 ], uint32_t n, uint32_t const y[ 8 ] ) {
+  uint64_t cx = 0, cy = 0; uint32_t br = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) {
+    uint64_t px = (uint64_t)m * x[j] + cx; cx = px >> 32;
+    uint64_t py = (uint64_t)n * y[j] + cy; cy = py >> 32;
+    uint64_t d = (uint64_t)(uint32_t)px - (uint32_t)py - br;
+    r[j] = (uint32_t)d; br = (uint32_t)(d >> 63);
+  }
+  r[8] = (uint32_t)cx - (uint32_t)cy - br;
+}
+
+/* r = neg ? -r : r (9 words), result known to fit 8 words */
+FD_LT_FN void lat_cneg( uint32_t o[ 8 ], uint32_t const r[ 9 ], int neg ) {
+  uint32_t msk = neg ? 0xffffffffu : 0u;
+  uint32_t c = neg ? 1u : 0u;
+#pragma unroll
+  for( int j=0; j<8; j++ ) { uint64_t t = (uint64_t)(r[j] ^ msk) + c; o[j] = (uint32_t)t; c = (uint32_t)(t >> 32); }
+}
+
+/* One Lehmer round (Lehmer 1938; exact-quotient test with interval bounds):
+   x > y >= 2^128.  The top 53 bits of x and the same bits of y (exact
+   truncations X, Y: x/2^e in [X, X+1)) drive Euclid in f64; a step is taken
+   only if its quotient is provably the true one given the truncation
+   error, and the round stops once the new remainder might be below 2^128
+   (the caller finishes the crossing exactly).  The accumulated 2x2
+   matrix is then applied to (x, y) and the cofactors (tx, ty).  Returns
+   the number of Euclid steps taken (0: no progress, take an exact step).
+   Sign bookkeeping: with x = s tx k, y = -s ty k (mod 8l) on entry, the
+   same holds on exit with s multiplied by (-1)^steps. */
+FD_LT_FN int lat_lehmer( uint32_t x[ 8 ], uint32_t tx[ 4 ], uint32_t y[ 8 ], uint32_t ty[ 4 ], int act ) {
+  int t = x[7] ? 7 : (x[6] ? 6 : (x[5] ? 5 : 4));
+  uint32_t xt = lat_word( x, t ), xt1 = lat_word( x, t-1 ), xt2 = lat_word( x, t-2 );
+  uint32_t yt = lat_word( y, t ), yt1 = lat_word( y, t-1 ), yt2 = lat_word( y, t-2 );
+  int c = xt ? __builtin_clz( xt ) : 0;
+  uint64_t X64 = ((((uint64_t)xt << 32) | xt1) << c) | (((uint64_t)xt2) >> (32 - c));
+  uint64_t Y64 = ((((uint64_t)yt << 32) | yt1) << c) | (((uint64_t)yt2) >> (32 - c));
+  double A = (double)(X64 >> 11), B = (double)(Y64 >> 11);
+  int e0 = 32*t - 21 - c;                            /* x ~ A 2^e0 */
+  double thr = ldexp( 1.0, 128 - e0 );               /* b >= 2^128  <=>  b/2^e0 >= thr */
+  double a0 = 1.0, a1 = 0.0, b0 = 0.0, b1 = 1.0;     /* magnitudes of the 2x2 matrix */
+  int j = 0;
+  int go = act;
+  while( lat_any( go ) ) {
+    if( go ) {
+      double q = floor( A * lat_rcp( B ) );
+      double R = fma( -q, B, A );
+      if( R < 0.0 ) { q -= 1.0; R += B; }
+      if( R >= B )  { q += 1.0; R -= B; }
+      double EA = a0 + a1, EB = b0 + b1;
+      double nb0 = fma( q, b0, a0 ), nb1 = fma( q, b1, a1 );
+      /* exact iff q <= true quotient < q+1 for every x/2^e0, y/2^e0 in
+         their truncation intervals; keep every quantity below 2^53 */
+      int ok = (R - EA - q*EB >= 0.0) && (B - R - EA - (q + 1.0)*EB > 0.0) && (nb0 + nb1 < 67108864.0);
+      if( ok ) {
+        A = B; B = R;
+        a0 = b0; a1 = b1; b0 = nb0; b1 = nb1;
+        j++;
+        /* stop once the new remainder might be < 2^128 (or shrank too far to steer) */
+        if( R - (nb0 + nb1) < thr || R < 67108864.0 ) go = 0;
+      } else go = 0;
     }
   }
-  if( act && !big ) {
-    uint32_t m = q < 1.0 ? 1u : (uint32_t)q;
-    lat_submul<4>( x, y, tx, ty, m, 0 );
+  if( act && j ) {
+    /* (x', y') = j even: (a0 x - a1 y, b1 y - b0 x); j odd: negated */
+    uint32_t ua0 = (uint32_t)a0, ua1 = (uint32_t)a1, ub0 = (uint32_t)b0, ub1 = (uint32_t)b1;
+    uint32_t rx[ 9 ], ry[ 9 ];
+    lat_mxny( rx, ua0, x, ua1, y );
+    lat_mxny( ry, ub1, y, ub0, x );
+    uint32_t ntx[ 4 ], nty[ 4 ];
+    uint64_t c1 = 0, c2 = 0;
+#pragma unroll
+    for( int i=0; i<4; i++ ) {
+      uint64_t p1 = (uint64_t)ua0 * tx[i] + c1; uint64_t p1b = (uint64_t)ua1 * ty[i] + (uint32_t)p1;
+      ntx[i] = (uint32_t)p1b; c1 = (p1 >> 32) + (p1b >> 32);
+      uint64_t p2 = (uint64_t)ub0 * tx[i] + c2; uint64_t p2b = (uint64_t)ub1 * ty[i] + (uint32_t)p2;
+      nty[i] = (uint32_t)p2b; c2 = (p2 >> 32) + (p2b >> 32);
+    }
+    lat_cneg( x, rx, j & 1 );
+    lat_cneg( y, ry, j & 1 );
+#pragma unroll
+    for( int i=0; i<4; i++ ) { tx[i] = ntx[i]; ty[i] = nty[i]; }
   }
-  /* the estimate undershot (quotient close to an integer, or big): repeat */
-  int more = act && lat_ge( x, y );
+  return act ? j : 0;
+}
+
+/* One exact Euclid step on x > y: x -= m y (f64 estimate, repeated until
+   x < y), then swap (x, tx) <-> (y, ty). */
+FD_LT_FN void lat_exact_step( uint32_t x[ 8 ], uint32_t tx[ 4 ], uint32_t y[ 8 ], uint32_t ty[ 4 ], int act ) {
+  int more = act;
   while( lat_any( more ) ) {
     if( more ) {
       int s; uint32_t m = lat_qest( lat_f64( x ), lat_f64( y ), &s );
@@ -208,37 +287,37 @@ FD_LT_FN void lat_reduce( uint32_t x[ 8 ], uint32_t tx[ 4 ], uint32_t const y[ 8
     }
     more = more && lat_ge( x, y );
   }
-  if( act ) xf = lat_f64_hi( x );
+  if( act ) {
+#pragma unroll
+    for( int j=0; j<8; j++ ) { uint32_t q = x[j]; x[j] = y[j]; y[j] = q; }
+#pragma unroll
+    for( int j=0; j<4; j++ ) { uint32_t q = tx[j]; tx[j] = ty[j]; ty[j] = q; }
+  }
 }
 
 /* Short lattice vector for k (8 LE words, k < l).  Outputs |u| and v (> 0)
-   as 8 LE words each and the sign of u.  Returns the number of half-steps
-   (>= FD_LAT_MAX_ITER means the fallback (k, 1) was taken).
+   as 8 LE words each and the sign of u.  Returns the number of rounds and
+   exact steps (>= FD_LAT_MAX_ITER means the fallback (k, 1) was taken).
 
-   Invariants: a tb + b ta = 8l; with the larger of (a, b) reduced by the
-   smaller in alternation (no register swap), the one just reduced is
-   r_{i+1} = (-1)^(i+1) t_{i+1} k (mod 8l) in Euclid's numbering, i.e. the
-   pair's signs alternate.  Any m in [1, floor(x/y)] keeps the invariants. */
+   Invariants: x > y, x tx... : x ty + y tx = 8l (Euclid's identity for
+   consecutive remainders), y = (-1)^par ty k and x = -(-1)^par tx k
+   (mod 8l); each Lehmer round takes j exact Euclid steps at once (par
+   advances by j), and the crossing below 2^128 is made by exact steps. */
 FD_LT_FN int lat_short_vector( uint32_t const k[ 8 ], uint32_t u[ 8 ], uint32_t v[ 8 ], int * u_neg ) {
-  uint32_t a[ 8 ] = { FD_N8L0, FD_N8L1, FD_N8L2, FD_N8L3, 0u, 0u, 0u, FD_N8L7 };
-  uint32_t b[ 8 ];
-  uint32_t ta[ 4 ] = { 0u, 0u, 0u, 0u }, tb[ 4 ] = { 1u, 0u, 0u, 0u };
+  uint32_t x[ 8 ] = { FD_N8L0, FD_N8L1, FD_N8L2, FD_N8L3, 0u, 0u, 0u, FD_N8L7 };
+  uint32_t y[ 8 ];
+  uint32_t tx[ 4 ] = { 0u, 0u, 0u, 0u }, ty[ 4 ] = { 1u, 0u, 0u, 0u };
 #pragma unroll
-  for( int j=0; j<8; j++ ) b[j] = k[j];
-  /* b = +tb k, a = -ta k (mod 8l) */
-  int active = (b[4] | b[5] | b[6] | b[7]) != 0u;   /* b >= 2^128: keep going */
-  int last = 1;                                     /* which of (a, b) holds r_i: 1 = b */
+  for( int j=0; j<8; j++ ) y[j] = k[j];
+  int par = 0;
+  int active = (y[4] | y[5] | y[6] | y[7]) != 0u;   /* y >= 2^128: keep going */
   int it = 0;
-  double af = 0.0, bf = 0.0;
-  if( active ) { af = lat_f64_hi( a ); bf = lat_f64_hi( b ); }
   while( lat_any( active ) ) {
-    /* a -= q b: now a = r_{i+1} < b */
-    lat_reduce( a, ta, b, tb, af, bf, active );
-    if( active ) { last = 0; it++; active = ((a[4] | a[5] | a[6] | a[7]) != 0u) && it < FD_LAT_MAX_ITER; }
-    if( !lat_any( active ) ) break;
-    /* b -= q a */
-    lat_reduce( b, tb, a, ta, bf, af, active );
-    if( active ) { last = 1; it++; active = ((b[4] | b[5] | b[6] | b[7]) != 0u) && it < FD_LAT_MAX_ITER; }
+    int jj = lat_lehmer( x, tx, y, ty, active );
+    par ^= jj & 1;
+    int need = active && jj == 0;
+    if( lat_any( need ) ) { lat_exact_step( x, tx, y, ty, need ); par ^= need; }
+    if( active ) { it++; active = ((y[4] | y[5] | y[6] | y[7]) != 0u) && it < FD_LAT_MAX_ITER; }
   }
   if( it >= FD_LAT_MAX_ITER ) {
 #pragma unroll
@@ -246,24 +325,15 @@ FD_LT_FN int lat_short_vector( uint32_t const k[ 8 ], uint32_t u[ 8 ], uint32_t 
     *u_neg = 0;
     return it;
   }
-  /* (r, tr) = the remainder below 2^128 and its cofactor, (p, tp) = the
-     previous remainder.  Sign: b-side values are +t k, a-side -t k; the
-     cofactor magnitudes tb, ta carry those signs ((-1)^par in the swapped
-     formulation: par = 1 when r sits in a). */
-  uint32_t r[ 8 ], p[ 8 ], tr[ 4 ], tp[ 4 ];
-#pragma unroll
-  for( int j=0; j<8; j++ ) { r[j] = last ? b[j] : a[j]; p[j] = last ? a[j] : b[j]; }
-#pragma unroll
-  for( int j=0; j<4; j++ ) { tr[j] = last ? tb[j] : ta[j]; tp[j] = last ? ta[j] : tb[j]; }
-  int par = !last;
-  if( tr[0] & 1u ) {
+  /* (r, tr) = (y, ty) the first remainder below 2^128, (p, tp) = (x, tx) */
+  if( ty[0] & 1u ) {
     /* (u, v) = (r, (-1)^par tr) */
 #pragma unroll
-    for( int j=0; j<8; j++ ) { u[j] = r[j]; v[j] = j < 4 ? tr[j] : 0u; }
+    for( int j=0; j<8; j++ ) { u[j] = y[j]; v[j] = j < 4 ? ty[j] : 0u; }
     *u_neg = par;
   } else {
     /* (u, v) = (p - j r, -(-1)^par (tp + j tr)), j ~ (p - tp) / (r + tr) */
-    double pf = lat_f64( p ), rf = lat_f64( r ), tpf = lat_f64_4( tp ), trf = lat_f64_4( tr );
+    double pf = lat_f64( x ), rf = lat_f64( y ), tpf = lat_f64_4( tx ), trf = lat_f64_4( ty );
     double jf = ((pf - tpf) / (rf + trf)) * (1.0 - 0x1p-40);
     uint32_t jj = jf < 1.0 ? 0u : (jf < 4294967295.0 ? (uint32_t)jf : 0xffffffffu);
     /* clamp to floor(p/r) (only matters if the estimate is off) */
@@ -271,11 +341,11 @@ FD_LT_FN int lat_short_vector( uint32_t const k[ 8 ], uint32_t u[ 8 ], uint32_t 
       int s; uint32_t mq = lat_qest( pf, rf, &s );
       if( s == 0 && mq < jj ) jj = mq;
     }
-    uint32_t t8[ 8 ] = { tp[0], tp[1], tp[2], tp[3], 0u, 0u, 0u, 0u };
-    uint32_t tr8[ 8 ] = { tr[0], tr[1], tr[2], tr[3], 0u, 0u, 0u, 0u };
-    if( jj ) lat_submul<8>( p, r, t8, tr8, jj, 0 );
+    uint32_t t8[ 8 ] = { tx[0], tx[1], tx[2], tx[3], 0u, 0u, 0u, 0u };
+    uint32_t tr8[ 8 ] = { ty[0], ty[1], ty[2], ty[3], 0u, 0u, 0u, 0u };
+    if( jj ) lat_submul<8>( x, y, t8, tr8, jj, 0 );
 #pragma unroll
-    for( int j=0; j<8; j++ ) { u[j] = p[j]; v[j] = t8[j]; }
+    for( int j=0; j<8; j++ ) { u[j] = x[j]; v[j] = t8[j]; }
     *u_neg = par ^ 1;
   }
   return it;

@@ -14,7 +14,7 @@ __global__ void __launch_bounds__(256) NAME(uint32_t* out, unsigned long long* c
   uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3; uint32_t a = threadIdx.x ^ seed, b = seed * 3u + 1u; \
   uint64_t t0 = __builtin_amdgcn_s_memtime();                                                     \
   for (int it = 0; it < iters; it++)                                                              \
-    asm volatile(BODY(I0, I1, I2, I3) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a), "v"(b) : "vcc"); \
+    asm volatile(BODY(I0, I1, I2, I3) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a), "v"(b) : "vcc", "s40", "s41"); \
   uint64_t t1 = __builtin_amdgcn_s_memtime();                                                     \
   uint32_t s = (uint32_t)(a0 ^ a1 ^ a2 ^ a3);                                                     \
   if ((threadIdx.x & 63) == 0) atomicAdd(cyc, (unsigned long long)(t1 - t0));                     \
@@ -24,7 +24,7 @@ __global__ void __launch_bounds__(256) NAME(uint32_t* out, unsigned long long* c
   uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3; uint32_t a = threadIdx.x ^ seed, b = seed * 3u + 1u; \
   uint64_t t0 = __builtin_amdgcn_s_memtime();                                                     \
   for (int it = 0; it < iters; it++)                                                              \
-    asm volatile(BODY(I0, I1, I2, I3) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a), "v"(b) : "vcc"); \
+    asm volatile(BODY(I0, I1, I2, I3) : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a), "v"(b) : "vcc", "s40", "s41"); \
   uint64_t t1 = __builtin_amdgcn_s_memtime();                                                     \
   uint32_t s = a0 ^ a1 ^ a2 ^ a3;                                                                 \
   if ((threadIdx.x & 63) == 0) atomicAdd(cyc, (unsigned long long)(t1 - t0));                     \
@@ -43,6 +43,10 @@ KERNEL32(k_adddpp, "v_add_u32_dpp %0, %4, %0 quad_perm:[1,0,3,2] row_mask:0xf ba
 KERNEL32(k_cnd64, "v_cndmask_b32_e64 %0, %0, %4, s[40:41]", "v_cndmask_b32_e64 %1, %1, %4, s[40:41]", "v_cndmask_b32_e64 %2, %2, %4, s[42:43]", "v_cndmask_b32_e64 %3, %3, %4, s[42:43]")
 KERNEL32(k_bfi,   "v_bfi_b32 %0, %4, %0, %5", "v_bfi_b32 %1, %4, %1, %5", "v_bfi_b32 %2, %4, %2, %5", "v_bfi_b32 %3, %4, %3, %5")
 KERNEL32(k_swap,  "v_permlane32_swap_b32 %0, %1", "v_permlane32_swap_b32 %2, %3", "v_permlane32_swap_b32 %1, %0", "v_permlane32_swap_b32 %3, %2")
+KERNEL32(k_cmpcnd, "v_cmp_lt_u32 vcc, %4, %0", "v_cndmask_b32 %1, %1, %0, vcc", "v_cndmask_b32 %2, %2, %1, vcc", "v_cndmask_b32 %3, %3, %2, vcc")
+KERNEL32(k_cmpcnd64, "v_cmp_lt_u32_e64 s[40:41], %4, %0", "v_cndmask_b32_e64 %1, %1, %0, s[40:41]", "v_cndmask_b32_e64 %2, %2, %1, s[40:41]", "v_cndmask_b32_e64 %3, %3, %2, s[40:41]")
+KERNEL32(k_cnd64vcc, "v_cndmask_b32_e64 %0, %0, %4, vcc", "v_cndmask_b32_e64 %1, %1, %4, vcc", "v_cndmask_b32_e64 %2, %2, %4, vcc", "v_cndmask_b32_e64 %3, %3, %4, vcc")
+KERNEL32(k_addco, "v_add_co_u32 %0, vcc, %4, %0", "v_addc_co_u32 %1, vcc, %4, %1, vcc", "v_add_co_u32 %2, vcc, %4, %2", "v_addc_co_u32 %3, vcc, %4, %3, vcc")
 typedef void (*kfn)(uint32_t*, unsigned long long*, uint32_t, int);
 int run(const char* name, kfn f, int w) {
   uint32_t* d; unsigned long long* c; CHECK(hipMalloc(&d, 4096)); CHECK(hipMalloc(&c, 8));
@@ -59,6 +63,7 @@ int main() {
     run("v_fma_f64", k_fma64, w);
     run("v_mov_b32_dpp quad_perm", k_dpp, w); run("v_add_u32_dpp quad_perm", k_adddpp, w); run("v_cndmask_b32_e64 sgpr", k_cnd64, w);
     run("v_bfi_b32", k_bfi, w); run("v_permlane32_swap", k_swap, w);
+    run("v_cmp(vcc)+3 v_cndmask_e32", k_cmpcnd, w); run("v_cndmask_b32_e64 vcc", k_cnd64vcc, w); run("v_add_co/v_addc_co vcc", k_addco, w); run("v_cmp(sgpr)+3 v_cndmask_e64", k_cmpcnd64, w);
   }
   return 0;
 }

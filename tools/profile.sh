@@ -8,10 +8,10 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 BENCH="bench.py --steps 10 --warmup 2 --no-cpu"
-timeout -k 10 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
+timeout -k 10 240 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $BENCH > $OUT/kt_bench.json 2> $OUT/kt.err
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2> $OUT/pmc_fetch.err
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2> $OUT/pmc_write.err
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $OUT/pmc_sq -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2> $OUT/pmc_sq.err
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_ANY --output-format csv -d $OUT/pmc_sq -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2> $OUT/pmc_sq.err
 timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/pmc_grbm -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2> $OUT/pmc_grbm.err
 echo done > $OUT/DONE

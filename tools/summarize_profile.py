@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""summarize_profile.py -- turn a tools/profile.sh output directory
+(gpurun_out/prof_<tag>) into the committed summaries under profiles/<tag>/:
+
+  kernel_stats.csv    rocprofv3 --kernel-trace --stats summary (verbatim)
+  bench.json          the bench.py line of the same tree (un-profiled run)
+  pmc_traffic.json    HBM bytes per verify-kernel launch from separate
+                      FETCH_SIZE / WRITE_SIZE passes, with the gfx950
+                      correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE x 2
+                      for 16-B/lane reads; WRITE_SIZE as is)
+  pmc_sq.json         SQ counters per launch and per wave (VALU instructions,
+                      wave cycles, waits), GRBM_GUI_ACTIVE effective clock
+  issue_probe.json    tools/issue_probe.hip output (per-instruction issue cost)
+
+Usage: summarize_profile.py gpurun_out/prof_r01 profiles/r01
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+
+def pmc(path, kernel="fd_ed25519_verify_kernel"):
+    rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"] == kernel]
+    by = {}
+    for r in rows:
+        d = by.setdefault(r["Dispatch_Id"], {"dur_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                                             "grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),
+                                             "lds": int(r["LDS_Block_Size"]), "scratch": int(r["Scratch_Size"])})
+        d[r["Counter_Name"]] = float(r["Counter_Value"])
+    return list(by.values())
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    json.dump(bench, open(os.path.join(dst, "bench.json"), "w"))
+    n = bench["config"]["batch_per_gpu"]
+
+    fe = pmc(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv"))
+    wr = pmc(os.path.join(src, "pmc_write", "pmc_counter_collection.csv"))
+    fetch_kb = statistics.median(d["FETCH_SIZE"] for d in fe)
+    write_kb = statistics.median(d["WRITE_SIZE"] for d in wr)
+    hbm = (2.0 * fetch_kb + write_kb) * 1024.0
+    traffic = {
+        "batch": n, "kernel": "fd_ed25519_verify_kernel", "launches": len(fe),
+        "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
+        "hbm_bytes_per_launch": hbm, "hbm_bytes_per_verify": hbm / n,
+        "note": "HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024, medians over the profiled launches of "
+                "separate --pmc passes; FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B "
+                "requests at 64 B; the kernel's dominant reads are 16-B/lane table loads)",
+    }
+    json.dump(traffic, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+
+    sq = pmc(os.path.join(src, "pmc_sq", "pmc_counter_collection.csv"))[-1]
+    gr = pmc(os.path.join(src, "pmc_grbm", "pmc_counter_collection.csv"))[-1]
+    waves = sq["SQ_WAVES"]
+    out = {k: v for k, v in sq.items()}
+    out.update({
+        "valu_instr_per_wave": sq["SQ_INSTS_VALU"] / waves,
+        "wave_cycles_per_wave": 4.0 * sq["SQ_WAVE_CYCLES"] / waves,
+        "wait_any_frac": sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"],
+        "cycles_per_valu_instr": 4.0 * sq["SQ_WAVE_CYCLES"] / sq["SQ_INSTS_VALU"],
+        "GRBM_GUI_ACTIVE": gr.get("GRBM_GUI_ACTIVE"),
+        "effective_clock_ghz": gr.get("GRBM_GUI_ACTIVE", 0) / 8.0 / gr["dur_ns"],
+        "note": "SQ_WAVE_CYCLES / SQ_WAIT_ANY count quad-cycles (x4 = cycles); one wave = 64 signatures",
+    })
+    json.dump(out, open(os.path.join(dst, "pmc_sq.json"), "w"), indent=1)
+
+    ip = os.path.join(src, "issue_probe.jsonl")
+    if os.path.exists(ip):
+        probes = [json.loads(l) for l in open(ip) if l.startswith("{")]
+        json.dump({"tool": "tools/issue_probe.hip", "probes": probes}, open(os.path.join(dst, "issue_probe.json"), "w"),
+                  indent=1)
+    print(json.dumps({"bench": bench["value"], "kernel_ms": bench["roofline"]["kernel_ms"],
+                      "hbm_bytes_per_launch": hbm, "valu_instr_per_wave": out["valu_instr_per_wave"],
+                      "cycles_per_valu_instr": out["cycles_per_valu_instr"]}))
+
+
+if __name__ == "__main__":
+    main()
