@@ -47,5 +47,6 @@ struct verify_args {
 #define FD_KERN_VERIFY   "fd_ed25519_verify_kernel"
 #define FD_KERN_BTAB     "fd_ed25519_btab_init"
 #define FD_KERN_LATTEST  "fd_ed25519_lattice_test_kernel"
+#define FD_KERN_SHA512   "fd_sha512_batch_kernel"
 
 #endif /* FD_ED25519_GPU_ABI_H */

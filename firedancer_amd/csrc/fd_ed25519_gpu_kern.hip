@@ -468,6 +468,66 @@ fd_ed25519_verify_kernel( verify_args args ) {
 #endif
 }
 
+/* ------------------------------------------------------------------ SHA-512 batch */
+
+/* Batched SHA-512, one message per lane (replaces fd_sha512_batch_init /
+   _add / _fini, src/ballet/sha512/fd_sha512.h:223-408, and fd_sha512_hash
+   fd_sha512.c:399).  Messages are (off, sz) pairs into one arena; digest i
+   goes to out[64 i .. 64 i + 63].  Each block's dwords are fetched one block
+   ahead (the fetch of block b covers message bytes [128 b, 128 b + 128) plus
+   the misalignment word). */
+__device__ __forceinline__ void sha_fetch_msg( uint32_t raw[ 33 ], uint32_t const * a32, uint32_t off, uint32_t b,
+                                               uint32_t lim_dw ) {
+  uint32_t start = (off >> 2) + 32u*b;
+#pragma unroll
+  for( int i=0; i<33; i++ ) raw[i] = a32[ min( start + (uint32_t)i, lim_dw ) ];
+}
+
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_sha512_batch_kernel( uint8_t const * arena, uint64_t arena_sz, fd_sha512_gpu_msg_t const * msg, uint64_t n,
+                        uint8_t * out ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  fd_sha512_gpu_msg_t m = msg[ i ];
+  uint32_t lim_dw = (uint32_t)((arena_sz + 3u) >> 2) + 1u;
+  uint32_t const * a32 = (uint32_t const *)arena;
+  uint32_t sz = m.sz, sh = m.off & 3u;
+  uint32_t nblk = (sz + 17u + 127u) >> 7;
+  uint64_t h[ 8 ]; sha512_init_state( h );
+  uint32_t nxt[ 33 ];
+  sha_fetch_msg( nxt, a32, m.off, 0u, lim_dw );
+  for( uint32_t b=0; b<nblk; b++ ) {
+    uint32_t raw[ 33 ];
+#pragma unroll
+    for( int j=0; j<33; j++ ) raw[j] = nxt[j];
+    if( b + 1u < nblk ) sha_fetch_msg( nxt, a32, m.off, b + 1u, lim_dw );
+    uint64_t W[ 16 ];
+#pragma unroll
+    for( int j=0; j<16; j++ ) {
+      int32_t mo = (int32_t)((b << 7) + 8u*(uint32_t)j);            /* message byte of the word's first byte */
+      uint32_t w0 = __builtin_amdgcn_alignbyte( raw[2*j+1], raw[2*j],   sh );
+      uint32_t w1 = __builtin_amdgcn_alignbyte( raw[2*j+2], raw[2*j+1], sh );
+      uint32_t hi = sha_bswap32( w0 ), lo = sha_bswap32( w1 );
+      int32_t rem0 = (int32_t)sz - mo, rem1 = rem0 - 4;
+      uint32_t keep0 = rem0 >= 4 ? 0xffffffffu : (rem0 <= 0 ? 0u : ~(0xffffffffu >> (8*rem0)));
+      uint32_t keep1 = rem1 >= 4 ? 0xffffffffu : (rem1 <= 0 ? 0u : ~(0xffffffffu >> (8*rem1)));
+      uint32_t pad0  = (rem0 >= 0 && rem0 < 4) ? (0x80000000u >> (8*rem0)) : 0u;
+      uint32_t pad1  = (rem1 >= 0 && rem1 < 4) ? (0x80000000u >> (8*rem1)) : 0u;
+      hi = (hi & keep0) | pad0;
+      lo = (lo & keep1) | pad1;
+      if( b == nblk-1u && j == 15 ) { hi = sz >> 29; lo = sz << 3; }
+      if( b == nblk-1u && j == 14 ) { hi = 0u; lo = 0u; }
+      W[j] = ((uint64_t)hi << 32) | lo;
+    }
+    sha512_compress( h, W );
+  }
+  uint4 * o = (uint4 *)(out + 64u*i);
+#pragma unroll
+  for( int q=0; q<4; q++ )
+    o[q] = make_uint4( sha_bswap32( (uint32_t)(h[2*q]   >> 32) ), sha_bswap32( (uint32_t)h[2*q]   ),
+                       sha_bswap32( (uint32_t)(h[2*q+1] >> 32) ), sha_bswap32( (uint32_t)h[2*q+1] ) );
+}
+
 /* Self-test kernel (tests only, fd_ed25519_gpu_test_lattice): the device
    lattice reduction on caller-supplied k, one per lane. */
 extern "C" __global__ void fd_ed25519_lattice_test_kernel( uint32_t const * k, uint32_t * out, uint64_t n ) {

@@ -16,6 +16,9 @@ GPU_PENDING = 1
 CODES_AVX512 = 0
 CODES_REF = 1
 
+# fd_sha512_gpu_msg_t (8 bytes)
+SHA_MSG_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4")])
+
 # fd_ed25519_desc_t (16 bytes, include/fd_ed25519_gpu.h)
 DESC_DTYPE = np.dtype([("sig_off", "<u4"), ("pub_off", "<u4"), ("msg_off", "<u4"),
                        ("msg_sz", "<u2"), ("txn_idx", "<u2")])
@@ -65,6 +68,8 @@ def load_lib():
     lib.fd_ed25519_gpu_txn_reduce.restype = ctypes.c_int64
     lib.fd_ed25519_gpu_txn_reduce.argtypes = [vp, vp, u64, vp, u64]
     lib.fd_ed25519_gpu_test_lattice.argtypes = [vp, vp, u64, vp]
+    lib.fd_sha512_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
+    lib.fd_sha512_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_strerror.restype = ctypes.c_char_p
     lib.fd_ed25519_gpu_strerror.argtypes = [i32]
     _LIB = lib
@@ -195,3 +200,26 @@ class Ed25519Gpu:
         if r:
             raise GpuError("fd_ed25519_gpu_test_lattice: %s (%d)" % (strerror(r), r))
         return out
+
+    def sha512_batch(self, msgs):
+        """Batched SHA-512 of a list of byte strings (mirror of fd_sha512_batch_add per message)."""
+        msgs = list(msgs)
+        total = sum(len(m) for m in msgs)
+        arena = np.zeros(total + 16, np.uint8)
+        desc = np.zeros(len(msgs), SHA_MSG_DTYPE)
+        off = 0
+        for i, m in enumerate(msgs):
+            if m:
+                arena[off:off + len(m)] = np.frombuffer(m, np.uint8)
+            desc[i] = (off, len(m))
+            off += len(m)
+        out = np.zeros(64 * max(len(msgs), 1), np.uint8)
+        r = self.lib.fd_sha512_batch_gpu(self.ctx, _ptr(arena), total, _ptr(desc), len(msgs), _ptr(out))
+        if r:
+            raise GpuError("fd_sha512_batch_gpu: %s (%d)" % (strerror(r), r))
+        return [out[64 * i:64 * i + 64].tobytes() for i in range(len(msgs))]
+
+    def sha512_batch_dev(self, d_arena, arena_sz, d_msg, msg_cnt, d_out, stream=0, dev_idx=0):
+        r = self.lib.fd_sha512_batch_gpu_dev(self.ctx, dev_idx, d_arena, arena_sz, d_msg, msg_cnt, d_out, stream)
+        if r:
+            raise GpuError("fd_sha512_batch_gpu_dev: %s (%d)" % (strerror(r), r))

@@ -130,6 +130,25 @@ int64_t fd_ed25519_gpu_txn_reduce( int8_t const * out_code, fd_ed25519_desc_t co
 
 char const * fd_ed25519_gpu_strerror( int err );
 
+/* Batched SHA-512 (replaces fd_sha512_batch_init/_add/_fini,
+   src/ballet/sha512/fd_sha512.h:223-408, i.e. fd_sha512_hash per message,
+   fd_sha512.c:399): message i is arena[msg[i].off, msg[i].off+msg[i].sz),
+   its 64-byte digest goes to out_hash[64 i, 64 i + 64).  Host memory,
+   synchronous, on the context's first device; messages outside the arena
+   -> FD_ED25519_GPU_ERR_ARG (nothing launched). */
+typedef struct {
+  uint32_t off;
+  uint32_t sz;
+} fd_sha512_gpu_msg_t;
+
+int fd_sha512_batch_gpu( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                         fd_sha512_gpu_msg_t const * msg, uint64_t msg_cnt, uint8_t * out_hash );
+
+/* Device-resident variant (enqueue only; d_arena readable up to
+   align_up(arena_sz,4)+8 bytes, d_out 64*msg_cnt bytes). */
+int fd_sha512_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx, uint8_t const * d_arena, uint64_t arena_sz,
+                             fd_sha512_gpu_msg_t const * d_msg, uint64_t msg_cnt, uint8_t * d_out, void * stream );
+
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
    u32 words each, k < l) on the context's first device.  out: n records of

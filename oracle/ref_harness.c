@@ -112,3 +112,42 @@ fdref_verify_descs( uchar const * arena, void const * desc, ulong n, schar * out
   for( ulong t=0UL; t<nthreads; t++ ) pthread_join( tid[ t ], NULL );
   return 0;
 }
+
+/* Multi-threaded SHA-512 sweep with the reference fd_sha512_hash
+   (src/ballet/sha512/fd_sha512.c:399): the CPU baseline of
+   tools/bench_sha512.py.  msg = n (off, sz) u32 pairs into arena. */
+
+typedef struct {
+  uchar const * arena;
+  uint const *  msg;
+  ulong         lo, hi, passes;
+  uchar *       out;
+} fdref_sha_job_t;
+
+static void *
+fdref_sha_worker( void * _job ) {
+  fdref_sha_job_t * job = (fdref_sha_job_t *)_job;
+  for( ulong p=0UL; p<job->passes; p++ )
+    for( ulong i=job->lo; i<job->hi; i++ )
+      fd_sha512_hash( job->arena + job->msg[ 2UL*i ], job->msg[ 2UL*i+1UL ], job->out + 64UL*i );
+  return NULL;
+}
+
+int
+fdref_sha512_msgs( uchar const * arena, void const * msg, ulong n, uchar * out, ulong nthreads, ulong passes ) {
+  if( nthreads<1UL ) nthreads = 1UL;
+  if( nthreads>256UL ) nthreads = 256UL;
+  pthread_t       tid[ 256 ];
+  fdref_sha_job_t job[ 256 ];
+  for( ulong t=0UL; t<nthreads; t++ ) {
+    job[ t ].arena  = arena;
+    job[ t ].msg    = (uint const *)msg;
+    job[ t ].lo     = t*n/nthreads;
+    job[ t ].hi     = (t+1UL)*n/nthreads;
+    job[ t ].passes = passes;
+    job[ t ].out    = out;
+    if( pthread_create( &tid[ t ], NULL, fdref_sha_worker, &job[ t ] ) ) return -1;
+  }
+  for( ulong t=0UL; t<nthreads; t++ ) pthread_join( tid[ t ], NULL );
+  return 0;
+}
