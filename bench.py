@@ -10,8 +10,9 @@ own 64K batch: weak scaling, no collective on the data path (signatures are
 independent; the barrier + MAX-over-ranks timing is the only exchange).
 
 Synthetic data: 65,536 distinct keys and 200-byte random messages per rank
-(fixed seed), signed on the host by the reference fd_ed25519_sign compiled
-from the reference sources (oracle/_ref), one arena record per signature.
+(fixed seed), RFC 8032-signed on the host by the benchmark input generator
+tools/synth.py (our own code; the oracle is used only by cpu_baseline), one
+arena record per signature.
 
 Extra keys beside the contract fields:
   roofline     -- INT32 VALU multiply-add roofline of the verify kernel
@@ -45,61 +46,23 @@ NOMINAL_GHZ = 2.4
 N_CU = 256
 
 
-def _ref_signer():
-    """The reference fd_ed25519_sign / public_from_private (oracle/_ref, built
-    from the reference sources in the dev container; test/bench infrastructure)."""
-    path = os.path.join(REPO, "oracle", "_ref", "libfdref_avx512.so")
-    if not os.path.exists(path):
-        path = os.path.join(REPO, "oracle", "_ref", "libfdref_ref.so")
-    if not os.path.exists(path):
-        return None
-    lib = ctypes.CDLL(path)
-    lib.fdref_public_from_private.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
-    lib.fdref_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
-    return lib
-
-
 def build_workload(n, msg_sz, seed):
-    """n DISTINCT reference-signed signatures (fresh key + msg_sz random bytes each,
-    fixed seed), signed on the host by the reference fd_ed25519_sign in 16 threads.
-    Falls back to tiling the 1024 committed config-1 signatures only if the
-    reference library is missing."""
+    """n DISTINCT signatures (fresh key + msg_sz random bytes each, fixed seed),
+    signed with RFC 8032 by the benchmark input generator tools/synth.py
+    ([s]B in tools/bin/libsynth_sign.so on 16 host threads; pinned against
+    the reference signer by tests/test_verify_stage.py)."""
     import firedancer_amd as fa
-    ref = _ref_signer()
-    if ref is None:
-        from golden_io import read_sigs
-        base = [r for r in read_sigs("synthetic.bin") if r["set"] == 10]
-        if msg_sz != 200:
-            raise SystemExit("reference signer missing: only the 200-byte tiled workload is available")
-        rot = seed % len(base)
-        recs = [(base[(i + rot) % 1024]["msg"], base[(i + rot) % 1024]["sig"], base[(i + rot) % 1024]["pub"])
-                for i in range(n)]
-        arena, desc, sz = fa.pack_batch(recs)
-        return arena, desc, sz, "1024 reference-signed config-1 signatures tiled to %d descriptors" % n
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import synth
     rng = np.random.default_rng(1234 + seed)
-    privs = rng.bytes(32 * n)
-    msgs = rng.bytes(msg_sz * n)
-    pubs = [None] * n
-    sigs = [None] * n
-
-    def work(lo, hi):
-        for i in range(lo, hi):
-            priv = privs[32 * i:32 * i + 32]
-            msg = msgs[msg_sz * i:msg_sz * i + msg_sz]
-            pub = ctypes.create_string_buffer(32)
-            ref.fdref_public_from_private(pub, priv)
-            sig = ctypes.create_string_buffer(64)
-            ref.fdref_sign(sig, msg, msg_sz, pub.raw, priv)
-            pubs[i] = pub.raw
-            sigs[i] = sig.raw
-    from concurrent.futures import ThreadPoolExecutor
-    nt = 16
-    with ThreadPoolExecutor(nt) as ex:
-        list(ex.map(lambda t: work(n * t // nt, n * (t + 1) // nt), range(nt)))
-    recs = [(msgs[msg_sz * i:msg_sz * i + msg_sz], sigs[i], pubs[i]) for i in range(n)]
+    seeds = [rng.bytes(32) for _ in range(n)]
+    msgs = [rng.bytes(msg_sz) for _ in range(n)]
+    kps = synth.keypairs(seeds, threads=16)
+    sigs = synth.sign_many([(s_, p_, m_) for (s_, p_), m_ in zip(kps, msgs)], threads=16)
+    recs = [(m_, g_, p_) for m_, g_, (_, p_) in zip(msgs, sigs, kps)]
     arena, desc, sz = fa.pack_batch(recs)
-    return arena, desc, sz, "%d distinct keys and %d-B random messages (seed %d), signed by the reference " \
-                            "fd_ed25519_sign (oracle/_ref), all valid" % (n, msg_sz, 1234 + seed)
+    return arena, desc, sz, "%d distinct keys and %d-B random messages (seed %d), RFC 8032-signed by " \
+                            "tools/synth.py, all valid" % (n, msg_sz, 1234 + seed)
 
 
 def valu_peak():

@@ -16,3 +16,7 @@ from .ed25519 import (  # noqa: F401
     CODES_AVX512, CODES_REF, DESC_DTYPE, SHA_MSG_DTYPE, Ed25519Gpu, GpuError, lib_path, load_lib, pack_batch,
     strerror, txn_reduce,
 )
+from .verify_stage import (  # noqa: F401
+    FD_TXN_VERIFY_BAD_FRAG, FD_TXN_VERIFY_DEDUP, FD_TXN_VERIFY_FAILED, FD_TXN_VERIFY_SUCCESS, FRAG_DTYPE, TCache,
+    VerifyStage, frags_to_descs,
+)

@@ -70,6 +70,19 @@ def load_lib():
     lib.fd_ed25519_gpu_test_lattice.argtypes = [vp, vp, u64, vp]
     lib.fd_sha512_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
     lib.fd_sha512_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_tcache_new.restype = vp
+    lib.fd_ed25519_gpu_tcache_new.argtypes = [u64, u64]
+    lib.fd_ed25519_gpu_tcache_delete.argtypes = [vp]
+    lib.fd_ed25519_gpu_tcache_reset.argtypes = [vp]
+    lib.fd_ed25519_gpu_tcache_depth.restype = u64
+    lib.fd_ed25519_gpu_tcache_depth.argtypes = [vp]
+    lib.fd_ed25519_gpu_tcache_map_cnt.restype = u64
+    lib.fd_ed25519_gpu_tcache_map_cnt.argtypes = [vp]
+    lib.fd_ed25519_gpu_tcache_query.argtypes = [vp, u64]
+    lib.fd_ed25519_gpu_tcache_insert.argtypes = [vp, u64]
+    lib.fd_ed25519_gpu_frags_to_descs.restype = ctypes.c_int64
+    lib.fd_ed25519_gpu_frags_to_descs.argtypes = [vp, u64, vp, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_verify_frags.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_strerror.restype = ctypes.c_char_p
     lib.fd_ed25519_gpu_strerror.argtypes = [i32]
     _LIB = lib

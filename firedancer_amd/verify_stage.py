@@ -1,0 +1,105 @@
+"""ctypes mirror of the verify-stage part of include/fd_ed25519_gpu.h
+(SURVEY.md §8(f) next-1 / next-2): the verify tile's per-frag logic,
+src/app/fdctl/run/tiles/fd_verify.c:76-124 (after_frag) and fd_txn_verify,
+src/app/fdctl/run/tiles/fd_verify.h:43-88, over batches of tango frags.
+
+  TCache        fd_tcache semantics (src/tango/tcache/fd_tcache.h), host side
+  frags_to_descs  frag layout -> signature descriptors (host only, no GPU)
+  VerifyStage   Ed25519Gpu + TCache: verify_frags(arena, frags) -> per-frag
+                FD_TXN_VERIFY_* results and the tile's opt_sig (the dedup tag)
+"""
+import numpy as np
+
+from .ed25519 import DESC_DTYPE, Ed25519Gpu, GpuError, _ptr, load_lib, strerror
+
+FD_TXN_VERIFY_SUCCESS = 0
+FD_TXN_VERIFY_FAILED = -1
+FD_TXN_VERIFY_DEDUP = -2
+FD_TXN_VERIFY_BAD_FRAG = -64
+
+VERIFY_TCACHE_DEPTH = 16    # src/app/fdctl/run/tiles/fd_verify.h:6
+VERIFY_TCACHE_MAP_CNT = 64  # src/app/fdctl/run/tiles/fd_verify.h:7
+
+# fd_ed25519_gpu_frag_t (8 bytes): frag i = arena[off, off+sz)
+FRAG_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4")])
+
+
+class TCache:
+    """fd_tcache with the tile's parameters by default (depth 16, map_cnt 64)."""
+
+    def __init__(self, depth=VERIFY_TCACHE_DEPTH, map_cnt=VERIFY_TCACHE_MAP_CNT):
+        self.lib = load_lib()
+        self.tc = self.lib.fd_ed25519_gpu_tcache_new(depth, map_cnt)
+        if not self.tc:
+            raise ValueError("bad tcache depth / map_cnt (%d, %d)" % (depth, map_cnt))
+
+    def close(self):
+        if self.tc:
+            self.lib.fd_ed25519_gpu_tcache_delete(self.tc)
+            self.tc = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def depth(self):
+        return int(self.lib.fd_ed25519_gpu_tcache_depth(self.tc))
+
+    @property
+    def map_cnt(self):
+        return int(self.lib.fd_ed25519_gpu_tcache_map_cnt(self.tc))
+
+    def reset(self):
+        self.lib.fd_ed25519_gpu_tcache_reset(self.tc)
+
+    def query(self, tag):
+        """FD_TCACHE_QUERY: True if tag is present."""
+        return bool(self.lib.fd_ed25519_gpu_tcache_query(self.tc, int(tag)))
+
+    def insert(self, tag):
+        """FD_TCACHE_INSERT: returns the dup flag."""
+        return bool(self.lib.fd_ed25519_gpu_tcache_insert(self.tc, int(tag)))
+
+
+def frags_to_descs(arena, arena_sz, frags):
+    """-> (desc DESC_DTYPE[n], frag_status int8[m], frag_tag uint64[m])."""
+    lib = load_lib()
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    frags = np.ascontiguousarray(frags, dtype=FRAG_DTYPE)
+    m = len(frags)
+    desc = np.zeros(max(16 * m, 1), DESC_DTYPE)
+    st = np.zeros(max(m, 1), np.int8)
+    tag = np.zeros(max(m, 1), np.uint64)
+    n = lib.fd_ed25519_gpu_frags_to_descs(_ptr(arena), arena_sz, _ptr(frags), m, _ptr(desc), len(desc), _ptr(st),
+                                          _ptr(tag))
+    if n < 0:
+        raise GpuError("fd_ed25519_gpu_frags_to_descs: %s (%d)" % (strerror(n), n))
+    return desc[:n].copy(), st[:m].copy(), tag[:m].copy()
+
+
+class VerifyStage:
+    """One verify tile's worth of state: a GPU verify context and its tcache."""
+
+    def __init__(self, gpu=None, tcache=None, **gpu_kw):
+        self.gpu = gpu if gpu is not None else Ed25519Gpu(**gpu_kw)
+        self.tcache = tcache if tcache is not None else TCache()
+
+    def verify_frags(self, arena, arena_sz, frags):
+        """-> (result int8[m] FD_TXN_VERIFY_*, sig uint64[m])."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        frags = np.ascontiguousarray(frags, dtype=FRAG_DTYPE)
+        m = len(frags)
+        res = np.zeros(max(m, 1), np.int8)
+        sig = np.zeros(max(m, 1), np.uint64)
+        r = self.gpu.lib.fd_ed25519_gpu_verify_frags(self.gpu.ctx, self.tcache.tc, _ptr(arena), arena_sz,
+                                                     _ptr(frags), m, _ptr(res), _ptr(sig))
+        if r:
+            raise GpuError("fd_ed25519_gpu_verify_frags: %s (%d)" % (strerror(r), r))
+        return res[:m].copy(), sig[:m].copy()
+
+    def close(self):
+        self.gpu.close()
+        self.tcache.close()

@@ -149,6 +149,72 @@ int fd_sha512_batch_gpu( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t
 int fd_sha512_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx, uint8_t const * d_arena, uint64_t arena_sz,
                              fd_sha512_gpu_msg_t const * d_msg, uint64_t msg_cnt, uint8_t * d_out, void * stream );
 
+/* ---- Verify stage ---------------------
+
+   The verify tile's per-frag logic (src/app/fdctl/run/tiles/fd_verify.c:
+   76-124 after_frag + fd_txn_verify, src/app/fdctl/run/tiles/fd_verify.h:
+   43-88) over a batch of frags: descriptor extraction from the tango frag
+   layout, one GPU batch verify, then the ha-dedup tcache steps replayed in
+   frag order, so results and tcache state equal the sequential tile's. */
+
+/* Per-frag results (src/app/fdctl/run/tiles/fd_verify.h:9-11) */
+#define FD_TXN_VERIFY_SUCCESS   ( 0)
+#define FD_TXN_VERIFY_FAILED    (-1)
+#define FD_TXN_VERIFY_DEDUP     (-2)
+/* A frag the tile would FD_LOG_ERR on (fd_verify.c:94-115: sz < 2, trailing
+   payload_sz > FD_TPU_DCACHE_MTU, recent_blockhash_off >= payload_sz), or
+   whose txn / signature / pubkey spans fall outside the arena. */
+#define FD_TXN_VERIFY_BAD_FRAG  (-64)
+
+/* One frag = arena[off, off+sz): the transaction payload, pad to 2-byte
+   alignment, the parsed fd_txn_t, then the u16 payload_sz in the last two
+   bytes (src/disco/quic/fd_tpu_reasm.c:175-221).  off/sz are what the
+   mcache frag's chunk/sz address (fd_chunk_to_laddr(mem,chunk) - arena). */
+typedef struct {
+  uint32_t off;
+  uint32_t sz;
+} fd_ed25519_gpu_frag_t;
+
+/* ha-dedup tag cache with fd_tcache semantics (src/tango/tcache/fd_tcache.h:
+   fd_tcache_new :176, FD_TCACHE_QUERY :281, FD_TCACHE_INSERT :373,
+   fd_tcache_remove :306, fd_tcache_reset :238).  depth > 0; map_cnt a power
+   of two >= depth+2, or 0 for fd_tcache_map_cnt_default.  The verify tile
+   uses depth 16, map_cnt 64 (fd_verify.h:6-7).  new returns NULL on bad
+   parameters.  query returns 1 if tag is present (the tag 0 always is);
+   insert returns the dup flag of FD_TCACHE_INSERT. */
+typedef struct fd_ed25519_gpu_tcache fd_ed25519_gpu_tcache_t;
+
+fd_ed25519_gpu_tcache_t * fd_ed25519_gpu_tcache_new( uint64_t depth, uint64_t map_cnt );
+void     fd_ed25519_gpu_tcache_delete ( fd_ed25519_gpu_tcache_t * tc );
+void     fd_ed25519_gpu_tcache_reset  ( fd_ed25519_gpu_tcache_t * tc );
+uint64_t fd_ed25519_gpu_tcache_depth  ( fd_ed25519_gpu_tcache_t const * tc );
+uint64_t fd_ed25519_gpu_tcache_map_cnt( fd_ed25519_gpu_tcache_t const * tc );
+int      fd_ed25519_gpu_tcache_query  ( fd_ed25519_gpu_tcache_t const * tc, uint64_t tag );
+int      fd_ed25519_gpu_tcache_insert ( fd_ed25519_gpu_tcache_t * tc, uint64_t tag );
+
+/* Host-only descriptor extraction (fd_verify.c:92-115 checks + the field
+   reads of fd_verify.h:49-60).  For frag i: frag_status[i] = 0 and its
+   signature_cnt descriptors appended to desc (txn_idx = i mod 2^16, in
+   signature order), or FD_TXN_VERIFY_FAILED (signature_cnt 0 or > 16: the
+   reference batch verify returns ERR_SIG without reading them), or
+   FD_TXN_VERIFY_BAD_FRAG.  frag_tag[i] = ha_dedup_tag (first 8 bytes of
+   signature 0, little-endian) for every frag not BAD (0 otherwise).
+   Returns the descriptor count, or FD_ED25519_GPU_ERR_ARG if desc_cap is
+   too small (16 * frag_cnt always suffices). */
+int64_t fd_ed25519_gpu_frags_to_descs( uint8_t const * arena, uint64_t arena_sz,
+                                       fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt,
+                                       fd_ed25519_desc_t * desc, uint64_t desc_cap,
+                                       int8_t * frag_status, uint64_t * frag_tag );
+
+/* The whole stage over frag_cnt frags in arrival order (host memory,
+   synchronous): result[i] = FD_TXN_VERIFY_*; sig_out[i] = the frag's
+   ha_dedup_tag when result[i] is SUCCESS (the tile's *opt_sig), else 0.
+   tc carries the dedup state across calls like the tile's tcache. */
+int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,
+                                 uint8_t const * arena, uint64_t arena_sz,
+                                 fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt,
+                                 int8_t * result, uint64_t * sig_out );
+
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
    u32 words each, k < l) on the context's first device.  out: n records of

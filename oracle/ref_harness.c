@@ -151,3 +151,113 @@ fdref_sha512_msgs( uchar const * arena, void const * msg, ulong n, uchar * out, 
   for( ulong t=0UL; t<nthreads; t++ ) pthread_join( tid[ t ], NULL );
   return 0;
 }
+
+/* ---- verify stage ------------------------
+
+   fdref_txn_parse: the reference fd_txn_parse (src/ballet/txn/fd_txn.h:656,
+   fd_txn_parse.c) -- used by the tests to build the [payload][pad][fd_txn_t]
+   [u16 payload_sz] frags exactly as fd_tpu_reasm's append_descriptor
+   (src/disco/quic/fd_tpu_reasm.c:175-221) lays them out.
+
+   fdref_verify_frags_seq: the verify tile's per-frag sequence over n frags
+   in order -- the after_frag checks (src/app/fdctl/run/tiles/fd_verify.c:
+   92-115) and fd_txn_verify (src/app/fdctl/run/tiles/fd_verify.h:43-88),
+   restated here line for line because fd_verify.h drags in the whole fdctl
+   build, over the REFERENCE tcache (FD_TCACHE_QUERY / FD_TCACHE_INSERT,
+   src/tango/tcache/fd_tcache.h) and the REFERENCE
+   fd_ed25519_verify_batch_single_msg.  result[i]: 0 SUCCESS, -1 FAILED,
+   -2 DEDUP (fd_verify.h:9-11), -64 a frag the tile would FD_LOG_ERR on. */
+
+#include "tango/tcache/fd_tcache.h"
+#include "ballet/txn/fd_txn.h"
+#include <stdlib.h>
+
+#define FDREF_TPU_DCACHE_MTU (2086UL) /* FD_TPU_DCACHE_MTU, src/disco/fd_disco_base.h:31,35 */
+
+ulong
+fdref_txn_parse( uchar const * payload, ulong payload_sz, void * out_buf ) {
+  return fd_txn_parse( payload, payload_sz, out_buf, NULL );
+}
+
+int
+fdref_verify_frags_seq( uchar const * arena, uint const * frags /* (off, sz) pairs */, ulong n,
+                        ulong depth, ulong map_cnt, schar * result, ulong * tag_out ) {
+  ulong footprint = fd_tcache_footprint( depth, map_cnt );
+  if( !footprint ) return -1;
+  void * mem = aligned_alloc( fd_tcache_align(), footprint );
+  if( !mem ) return -1;
+  fd_tcache_t * tcache = fd_tcache_join( fd_tcache_new( mem, depth, map_cnt ) );
+  ulong * sync = fd_tcache_oldest_laddr( tcache );
+  ulong * ring = fd_tcache_ring_laddr( tcache );
+  ulong * map  = fd_tcache_map_laddr( tcache );
+  ulong   tdepth = fd_tcache_depth( tcache ), tmap_cnt = fd_tcache_map_cnt( tcache );
+  *sync = fd_tcache_reset( ring, tdepth, map, tmap_cnt );
+  fd_sha512_t   _sha[ 16 ];
+  fd_sha512_t * shas[ 16 ];
+  for( ulong j=0UL; j<16UL; j++ ) shas[ j ] = fd_sha512_join( fd_sha512_new( &_sha[ j ] ) );
+
+  for( ulong i=0UL; i<n; i++ ) {
+    uchar const * udp_payload = arena + frags[ 2UL*i ];
+    ulong         sz          = frags[ 2UL*i+1UL ];
+    tag_out[ i ] = 0UL;
+    if( sz < sizeof(ushort) ) { result[ i ] = -64; continue; }                       /* fd_verify.c:94-96 */
+    ushort payload_sz = *(ushort const *)(udp_payload + sz - sizeof(ushort));        /* :98 */
+    if( payload_sz > FDREF_TPU_DCACHE_MTU ) { result[ i ] = -64; continue; }          /* :101-103 */
+    fd_txn_t const * txn = (fd_txn_t const *)fd_ulong_align_up( (ulong)udp_payload + payload_sz, 2UL ); /* :108 */
+    if( txn->recent_blockhash_off >= payload_sz ) { result[ i ] = -64; continue; }    /* :112-115 */
+
+    /* fd_txn_verify (fd_verify.h:43-88) */
+    uchar  signature_cnt = txn->signature_cnt;
+    ushort signature_off = txn->signature_off;
+    ushort acct_addr_off = txn->acct_addr_off;
+    ushort message_off   = txn->message_off;
+    uchar const * signatures = udp_payload + signature_off;
+    uchar const * pubkeys    = udp_payload + acct_addr_off;
+    uchar const * msg        = udp_payload + message_off;
+    ulong msg_sz = (ulong)payload_sz - message_off;
+    ulong ha_dedup_tag = *((ulong const *)signatures);
+    int   ha_dup;
+    ulong tcache_map_idx = 0;
+    FD_TCACHE_QUERY( ha_dup, tcache_map_idx, map, tmap_cnt, ha_dedup_tag );
+    (void)tcache_map_idx;
+    if( ha_dup ) { result[ i ] = -2; continue; }
+    int res = fd_ed25519_verify_batch_single_msg( msg, msg_sz, signatures, pubkeys, shas, signature_cnt );
+    if( res != FD_ED25519_SUCCESS ) { result[ i ] = -1; continue; }
+    FD_TCACHE_INSERT( ha_dup, *sync, ring, tdepth, map, tmap_cnt, ha_dedup_tag );
+    if( ha_dup ) { result[ i ] = -2; continue; }
+    tag_out[ i ] = ha_dedup_tag;
+    result[ i ] = 0;
+  }
+  free( fd_tcache_delete( fd_tcache_leave( tcache ) ) );
+  return 0;
+}
+
+/* fdref_tcache_seq: ops[i] = (kind, tag) with kind 0 = FD_TCACHE_QUERY,
+   1 = FD_TCACHE_INSERT on the REFERENCE tcache; out[i] = found / dup flag.
+   Final map (map_cnt u64) and ring (depth u64) + oldest copied out, so the
+   restatement's state can be compared slot for slot. */
+int
+fdref_tcache_seq( ulong depth, ulong map_cnt, ulong const * ops, ulong n, int * out,
+                  ulong * map_out, ulong * ring_out, ulong * oldest_out ) {
+  ulong footprint = fd_tcache_footprint( depth, map_cnt );
+  if( !footprint ) return -1;
+  void * mem = aligned_alloc( fd_tcache_align(), footprint );
+  if( !mem ) return -1;
+  fd_tcache_t * tcache = fd_tcache_join( fd_tcache_new( mem, depth, map_cnt ) );
+  ulong * sync = fd_tcache_oldest_laddr( tcache );
+  ulong * ring = fd_tcache_ring_laddr( tcache );
+  ulong * map  = fd_tcache_map_laddr( tcache );
+  ulong   tdepth = fd_tcache_depth( tcache ), tmap_cnt = fd_tcache_map_cnt( tcache );
+  for( ulong i=0UL; i<n; i++ ) {
+    ulong kind = ops[ 2UL*i ], tag = ops[ 2UL*i+1UL ];
+    int r; ulong idx;
+    if( kind==0UL ) { FD_TCACHE_QUERY( r, idx, map, tmap_cnt, tag ); (void)idx; }
+    else            { FD_TCACHE_INSERT( r, *sync, ring, tdepth, map, tmap_cnt, tag ); }
+    out[ i ] = r;
+  }
+  for( ulong j=0UL; j<tmap_cnt; j++ ) map_out[ j ] = map[ j ];
+  for( ulong j=0UL; j<tdepth;   j++ ) ring_out[ j ] = ring[ j ];
+  *oldest_out = *sync;
+  free( fd_tcache_delete( fd_tcache_leave( tcache ) ) );
+  return (int)tmap_cnt;
+}

@@ -1,0 +1,319 @@
+"""Verify stage: tcache, frag -> descriptor
+extraction and the whole per-frag verify over batches of tango frags.
+
+Oracles:
+  * the reference verify-tile test's transactions and assertions
+    (src/app/fdctl/run/tiles/test_verify.c:4-109 data, :144-264 FD_TESTs),
+    committed as tests/golden/verify_txns.json (make_verify_fixtures.py);
+  * the reference tile restated over the REFERENCE tcache and batch verify
+    (oracle/_ref fdref_verify_frags_seq / fdref_tcache_seq, ref_harness.c);
+  * the reference fd_txn_parse for the synthetic transactions' fd_txn_t.
+CPU tests need no GPU; the @gpu ones go through fd_ed25519_gpu_verify_frags.
+"""
+import ctypes
+import json
+import os
+import struct
+import sys
+
+import numpy as np
+import pytest
+
+import firedancer_amd as fa
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import synth  # noqa: E402
+
+REF_SO = os.path.join(REPO, "oracle", "_ref", "libfdref_avx512.so")
+S, F, D, BAD = fa.FD_TXN_VERIFY_SUCCESS, fa.FD_TXN_VERIFY_FAILED, fa.FD_TXN_VERIFY_DEDUP, fa.FD_TXN_VERIFY_BAD_FRAG
+
+
+@pytest.fixture(scope="module")
+def ref():
+    if not os.path.exists(REF_SO):
+        pytest.skip("oracle/_ref not built (needs /root/reference in the dev container)")
+    lib = ctypes.CDLL(REF_SO)
+    vp, ul = ctypes.c_void_p, ctypes.c_ulong
+    lib.fdref_verify_frags_seq.argtypes = [vp, vp, ul, ul, ul, vp, vp]
+    lib.fdref_tcache_seq.argtypes = [ul, ul, vp, ul, vp, vp, vp, vp]
+    lib.fdref_txn_parse.restype = ul
+    lib.fdref_txn_parse.argtypes = [ctypes.c_char_p, ul, ctypes.c_char_p]
+    lib.fdref_public_from_private.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    lib.fdref_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ul, ctypes.c_char_p, ctypes.c_char_p]
+    return lib
+
+
+def _vp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def ref_seq(ref, arena, frags, depth=16, map_cnt=64):
+    fr = np.ascontiguousarray(np.stack([frags["off"], frags["sz"]], 1).astype(np.uint32))
+    res = np.zeros(max(len(frags), 1), np.int8)
+    tag = np.zeros(max(len(frags), 1), np.uint64)
+    assert ref.fdref_verify_frags_seq(_vp(arena), _vp(fr), len(frags), depth, map_cnt, _vp(res), _vp(tag)) == 0
+    return res[:len(frags)], tag[:len(frags)]
+
+
+def fixture_txns():
+    d = json.load(open(os.path.join(REPO, "tests", "golden", "verify_txns.json")))["txns"]
+    return {k: (bytes.fromhex(v["payload"]), bytes.fromhex(v["txn_t"])) for k, v in d.items()}
+
+
+# ---- synthetic workload generator (tools/synth.py) pinned -----------------
+
+def test_synth_signer_rfc8032_vector():
+    """RFC 8032 7.1 TEST 1 (empty message)."""
+    seed = bytes.fromhex("9d61b19deffd5a60ba844af492ec2cc44449c5697b326919703bac031cae7f60")
+    (_, pub), = synth.keypairs([seed])
+    assert pub.hex() == "d75a980182b10ab7d54bfed3c964073a0ee172f3daa62325af021a68f707511a"
+    sig, = synth.sign_many([(seed, pub, b"")])
+    assert sig.hex() == ("e5564300c360ac729086e2cc806e828a84877f1eb8e5d974d873e06522490155"
+                         "5fb8821590a33bacc61e39701cf9b46bd25bf5f0595bbe24655141438e7a100b")
+
+
+def test_synth_signer_matches_reference(ref):
+    rng = np.random.default_rng(7)
+    seeds = [rng.bytes(32) for _ in range(64)]
+    kps = synth.keypairs(seeds, threads=4)
+    items = [(s, p, rng.bytes(int(rng.integers(0, 300)))) for s, p in kps]
+    sigs = synth.sign_many(items, threads=4)
+    for (s, p, m), sig in zip(items, sigs):
+        pub = ctypes.create_string_buffer(32)
+        ref.fdref_public_from_private(pub, s)
+        assert pub.raw == p
+        rs = ctypes.create_string_buffer(64)
+        ref.fdref_sign(rs, m, len(m), p, s)
+        assert rs.raw == sig
+
+
+@pytest.mark.parametrize("version", [synth.FD_TXN_VLEGACY, synth.FD_TXN_V0])
+def test_synth_txn_t_matches_reference_parser(ref, version):
+    rng = np.random.default_rng(11)
+    txns = synth.build_txns(rng, 10, list(range(1, 11)), threads=4, version=version, data_sz=16)
+    for payload, txn_t in txns:
+        buf = ctypes.create_string_buffer(852)
+        sz = ref.fdref_txn_parse(payload, len(payload), buf)
+        assert sz == len(txn_t)
+        assert buf.raw[:sz] == txn_t
+
+
+# ---- tcache ------------------------------------------------------------------
+
+@pytest.mark.parametrize("depth,map_cnt", [(16, 64), (5, 8), (1, 4), (16, 0), (100, 0), (30, 32)])
+def test_tcache_matches_reference(ref, depth, map_cnt):
+    """Random query / insert sequences over a small tag pool whose low bits
+    collide (long probe runs, wrap-around, backward-shift deletions, tag 0):
+    every found / dup flag equals the reference tcache's."""
+    rng = np.random.default_rng(depth * 1000 + map_cnt)
+    pool = [int(x) for x in rng.integers(0, 1 << 62, size=3 * depth + 8, dtype=np.int64)]
+    pool = [(t & ~0x7) | (i & 0x3) for i, t in enumerate(pool)] + [0, 8, 16, 24]
+    n = 4000
+    kinds = rng.integers(0, 4, size=n) != 0        # 3/4 inserts
+    tags = [pool[int(i)] for i in rng.integers(0, len(pool), size=n)]
+    ops = np.zeros((n, 2), np.uint64)
+    ops[:, 0] = kinds
+    ops[:, 1] = np.array(tags, np.uint64)
+    out = np.zeros(n, np.int32)
+    mapo = np.zeros(4096, np.uint64); ring = np.zeros(depth, np.uint64); oldest = np.zeros(1, np.uint64)
+    tmap = ref.fdref_tcache_seq(depth, map_cnt, _vp(ops), n, _vp(out), _vp(mapo), _vp(ring), _vp(oldest))
+    assert tmap > 0
+    tc = fa.TCache(depth, map_cnt)
+    assert tc.map_cnt == tmap and tc.depth == depth
+    mine = [int(tc.insert(t)) if k else int(tc.query(t)) for k, t in zip(kinds, tags)]
+    assert mine == [int(x) for x in out]
+    # final membership of every tag ever seen equals the reference map's
+    ref_set = set(int(x) for x in mapo[:tmap] if x)
+    for t in set(pool):
+        assert tc.query(t) == (t in ref_set or t == 0), t
+
+
+def test_tcache_params():
+    with pytest.raises(ValueError):
+        fa.TCache(0, 64)
+    with pytest.raises(ValueError):
+        fa.TCache(16, 48)      # not a power of two
+    with pytest.raises(ValueError):
+        fa.TCache(16, 16)      # < depth + 2
+    assert fa.TCache(16, 0).map_cnt == 64    # fd_tcache_map_cnt_default: 2^(msb(17)+2)
+    tc = fa.TCache(2, 4)
+    assert tc.query(0) and not tc.insert(7) and tc.insert(7)
+    assert not tc.insert(9) and not tc.insert(11)          # evicts 7
+    assert not tc.query(7) and tc.query(9) and tc.query(11)
+    tc.reset()
+    assert not tc.query(9)
+
+
+# ---- frag -> descriptors (host only) ------------------------------------
+
+def _mk_frags(txns):
+    return synth.pack_frags(txns)
+
+
+def test_frags_to_descs_fixture_txns():
+    fx = fixture_txns()
+    names = ["valid_txn_1sig", "valid_txn_2sigs", "invalid_txn_2sigs"]
+    arena, frags = _mk_frags([fx[k] for k in names])
+    desc, st, tag = fa.frags_to_descs(arena, len(arena), frags)
+    assert list(st) == [0, 0, 0]
+    assert len(desc) == 1 + 2 + 2
+    k = 0
+    for i, name in enumerate(names):
+        payload, txn_t = fx[name]
+        n, soff, moff = txn_t[1], struct.unpack_from("<H", txn_t, 2)[0], struct.unpack_from("<H", txn_t, 4)[0]
+        aoff = struct.unpack_from("<H", txn_t, 10)[0]
+        base = int(frags["off"][i])
+        assert int(tag[i]) == struct.unpack_from("<Q", payload, soff)[0]
+        for j in range(n):
+            d = desc[k]
+            assert (int(d["sig_off"]), int(d["pub_off"]), int(d["msg_off"]), int(d["msg_sz"]), int(d["txn_idx"])) == \
+                (base + soff + 64 * j, base + aoff + 32 * j, base + moff, len(payload) - moff, i)
+            k += 1
+
+
+def _corrupt_frags(arena, frags, kind, i):
+    """Edit frag i in place into one of the tile's sanity-check failures."""
+    off, sz = int(frags["off"][i]), int(frags["sz"][i])
+    psz = struct.unpack_from("<H", arena, off + sz - 2)[0]
+    t = off + psz + (psz & 1)
+    if kind == "short":
+        frags["sz"][i] = 1
+    elif kind == "mtu":
+        struct.pack_into("<H", arena, off + sz - 2, 2087)
+    elif kind == "rbh":
+        struct.pack_into("<H", arena, t + 12, psz)
+    elif kind == "nosig":
+        arena[t + 1] = 0
+    elif kind == "manysig":
+        arena[t + 1] = 17
+    elif kind == "outside":
+        frags["off"][i] = len(arena) - 4
+        frags["sz"][i] = 8
+
+
+def test_frags_to_descs_bad_frags():
+    fx = fixture_txns()
+    kinds = ["short", "mtu", "rbh", "nosig", "manysig", "outside", None]
+    arena, frags = _mk_frags([fx["valid_txn_1sig"]] * len(kinds))
+    for i, k in enumerate(kinds):
+        _corrupt_frags(arena, frags, k, i)
+    desc, st, tag = fa.frags_to_descs(arena, len(arena), frags)
+    assert list(st) == [BAD, BAD, BAD, F, F, BAD, 0]
+    assert len(desc) == 1 and int(desc[0]["txn_idx"]) == 6
+    assert int(tag[3]) == int(tag[6]) != 0
+
+
+def test_frags_reference_sanity_checks_agree(ref):
+    """Our per-frag BAD / FAILED classification equals the restated tile's
+    (reference tcache + reference verify) on the corrupted frags."""
+    fx = fixture_txns()
+    kinds = ["short", "mtu", "rbh", "nosig", "manysig", None]
+    arena, frags = _mk_frags([fx["valid_txn_1sig"]] * len(kinds))
+    for i, k in enumerate(kinds):
+        _corrupt_frags(arena, frags, k, i)
+    res, _ = ref_seq(ref, arena, frags)
+    _, st, _ = fa.frags_to_descs(arena, len(arena), frags)
+    assert list(res[:5]) == list(st[:5]) == [BAD, BAD, BAD, F, F]
+    assert res[5] == S
+
+
+# ---- the whole stage on the GPU -------------------------------------------
+
+TILE_SCENARIOS = [
+    # test_verify.c:144-186 test_verify_success
+    ([["valid_txn_2sigs"] * 3 + ["valid_txn_1sig"] * 3], [[S, D, D, S, D, D]]),
+    # :190-216 test_verify_invalid_sigs_success
+    ([["invalid_txn_2sigs"] * 2], [[F, F]]),
+    # :219-264 test_verify_invalid_dedup_success (tcache reset between the halves)
+    ([["invalid_txn_same_1sig", "valid_txn_1sig"], ["valid_txn_1sig", "invalid_txn_same_1sig"]], [[F, S], [S, D]]),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scenario", range(len(TILE_SCENARIOS)))
+@pytest.mark.parametrize("one_by_one", [False, True])
+def test_verify_frags_reference_tile_tests(gpu, scenario, one_by_one):
+    fx = fixture_txns()
+    tc = fa.TCache()
+    stage = fa.VerifyStage(gpu=gpu, tcache=tc)
+    halves, expect = TILE_SCENARIOS[scenario]
+    for names, exp in zip(halves, expect):
+        tc.reset()
+        arena, frags = _mk_frags([fx[k] for k in names])
+        if one_by_one:
+            got = []
+            for i in range(len(frags)):
+                r, _ = stage.verify_frags(arena, len(arena), frags[i:i + 1])
+                got.append(int(r[0]))
+        else:
+            r, sig = stage.verify_frags(arena, len(arena), frags)
+            got = [int(x) for x in r]
+            for i, name in enumerate(names):
+                pl = fx[name][0]
+                assert int(sig[i]) == (struct.unpack_from("<Q", pl, 1)[0] if got[i] == S else 0)
+        assert got == exp, (names, got, exp)
+
+
+def _random_frag_stream(rng, n_unique, n_total):
+    """n_unique synthetic txns (1..8 signers; a fifth with a corrupted
+    signature or message, some 'frontrun' copies reusing a valid txn's first
+    signature), then a stream of n_total frags drawn with repeats at short
+    and long distances (so duplicates hit, miss after eviction, and
+    invalid-first / valid-first orders both occur), plus sanity failures."""
+    cnts = [int(c) for c in rng.choice([1, 1, 1, 2, 2, 3, 4, 8], size=n_unique)]
+    txns = synth.build_txns(rng, n_unique, cnts, threads=16)
+    txns = [(bytearray(p), t) for p, t in txns]
+    extra = []
+    for i in range(n_unique):
+        r = rng.random()
+        p, t = txns[i]
+        if r < 0.10:
+            j = 1 + 64 * int(rng.integers(0, cnts[i])) + int(rng.integers(0, 64))
+            p[j] ^= 1 << int(rng.integers(0, 8))
+        elif r < 0.20:
+            mo = struct.unpack_from("<H", t, 4)[0]
+            j = mo + int(rng.integers(0, len(p) - mo))
+            p[j] ^= 1 << int(rng.integers(0, 8))
+        elif r < 0.28:
+            q = bytearray(p)   # frontrun: same first signature, different message
+            q[-1] ^= 0x5a
+            extra.append((bytes(q), t))
+    pool = [(bytes(p), t) for p, t in txns] + extra
+    order = []
+    for k in range(n_total):
+        r = rng.random()
+        if order and r < 0.25:
+            order.append(order[-int(rng.integers(1, min(len(order), 4) + 1))])      # near repeat
+        elif order and r < 0.35:
+            order.append(order[-int(rng.integers(1, len(order) + 1))])              # far repeat
+        else:
+            order.append(int(rng.integers(0, len(pool))))
+    arena, frags = synth.pack_frags([pool[i] for i in order])
+    kinds = ["short", "mtu", "rbh", "nosig", "manysig"]
+    for i in rng.choice(n_total, size=n_total // 50, replace=False):
+        _corrupt_frags(arena, frags, kinds[int(rng.integers(0, len(kinds)))], int(i))
+    return arena, frags
+
+
+@pytest.mark.gpu
+def test_verify_frags_random_stream_vs_reference_tile(gpu, ref):
+    """6000 frags in arrival order, fed in batches of 1, 7, 64, 500 and the
+    rest with the tcache carried across calls: results and opt_sig equal the
+    sequential reference tile's (reference tcache + reference verify)."""
+    rng = np.random.default_rng(2024)
+    arena, frags = _random_frag_stream(rng, 2500, 6000)
+    exp_res, exp_tag = ref_seq(ref, arena, frags)
+    stage = fa.VerifyStage(gpu=gpu, tcache=fa.TCache())
+    got_res, got_tag, i = [], [], 0
+    for b in [1, 7, 64, 500, len(frags)]:
+        r, s = stage.verify_frags(arena, len(arena), frags[i:i + b])
+        got_res.append(r); got_tag.append(s)
+        i += len(r)
+        if i >= len(frags):
+            break
+    got_res = np.concatenate(got_res); got_tag = np.concatenate(got_tag)
+    bad = np.nonzero((got_res != exp_res) | (got_tag != exp_tag))[0]
+    assert len(bad) == 0, [(int(j), int(got_res[j]), int(exp_res[j])) for j in bad[:10]]
+    hist = {int(k): int(v) for k, v in zip(*np.unique(exp_res, return_counts=True))}
+    assert hist.get(S, 0) > 1000 and hist.get(D, 0) > 300 and hist.get(F, 0) > 300 and hist.get(BAD, 0) > 30, hist

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""bench_verify_stage.py -- §8(f) next-1/next-2: the verify tile's whole
+per-frag logic on the GPU (fd_ed25519_gpu_verify_frags: frag -> descriptor
+extraction, one batch verify, in-order tcache replay), one JSON line.
+
+Workload: --frags frags (default 65,536) of synthetic signed Solana legacy
+transactions (tools/synth.py, fresh keys), signature counts drawn from
+{1 x5, 2 x2, 3, 4} (mean 1.8), --dup fraction of frags repeating an earlier
+one (HA duplicates), laid out [payload][pad][fd_txn_t][u16 sz] in 64-byte
+chunks like the dcache.  value = frags/s over the whole call from host
+memory (includes the arena / descriptor copies to HBM and the host-side
+parse and replay).  CPU baseline: the reference tile sequence
+(fdref_verify_frags_seq: reference tcache + fd_ed25519_verify_batch_single_msg,
+AVX-512 build) on ONE core -- the reference verify tile is single-threaded
+(fd_verify.c) -- over a bounded sample."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+
+def make_stream(n_frags, dup, seed=5):
+    import synth
+    rng = np.random.default_rng(seed)
+    n_unique = int(n_frags * (1.0 - dup))
+    cnts = [int(c) for c in rng.choice([1, 1, 1, 1, 1, 2, 2, 3, 4], size=n_unique)]
+    txns = synth.build_txns(rng, n_unique, cnts, threads=16)
+    order = list(range(n_unique))
+    for _ in range(n_frags - n_unique):
+        j = int(rng.integers(0, len(order)))
+        order.insert(j + int(rng.integers(1, 8)), order[j])
+    order = order[:n_frags]
+    arena, frags = synth.pack_frags([txns[i] for i in order])
+    return arena, frags, sum(cnts[i] for i in order)
+
+
+def cpu_baseline(arena, frags, budget_s=10.0):
+    path = os.path.join(REPO, "oracle", "_ref", "libfdref_avx512.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    vp, ul = ctypes.c_void_p, ctypes.c_ulong
+    lib.fdref_verify_frags_seq.argtypes = [vp, vp, ul, ul, ul, vp, vp]
+    m = min(len(frags), 8192)
+    fr = np.ascontiguousarray(np.stack([frags["off"][:m], frags["sz"][:m]], 1).astype(np.uint32))
+    res = np.zeros(m, np.int8); tag = np.zeros(m, np.uint64)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    t0 = time.perf_counter(); done = 0
+    while time.perf_counter() - t0 < budget_s:
+        lib.fdref_verify_frags_seq(p(arena), p(fr), m, 16, 64, p(res), p(tag))
+        done += m
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "frags/s", "cores": 1, "kind": "reference",
+            "sample": "%d passes over the first %d frags (%.1f s): reference tcache + "
+                      "fd_ed25519_verify_batch_single_msg (AVX-512 build), one thread like the tile" % (done // m, m, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frags", type=int, default=65536)
+    ap.add_argument("--dup", type=float, default=0.1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    import firedancer_amd as fa
+
+    t0 = time.perf_counter()
+    arena, frags, n_sigs = make_stream(args.frags, args.dup)
+    gen_s = time.perf_counter() - t0
+    g = fa.Ed25519Gpu(device_mask=1, max_batch=1 << 18)
+    stage = fa.VerifyStage(gpu=g, tcache=fa.TCache())
+    for _ in range(args.warmup):
+        stage.tcache.reset()
+        res, _ = stage.verify_frags(arena, len(arena), frags)
+    hist = {int(k): int(v) for k, v in zip(*np.unique(res, return_counts=True))}
+    t_parse = time.perf_counter()
+    for _ in range(3):
+        fa.frags_to_descs(arena, len(arena), frags)
+    parse_ms = (time.perf_counter() - t_parse) / 3 * 1e3
+    times = []
+    for _ in range(args.steps):
+        stage.tcache.reset()
+        t1 = time.perf_counter()
+        stage.verify_frags(arena, len(arena), frags)
+        times.append(time.perf_counter() - t1)
+    dt = float(np.mean(times))
+    line = {"metric": "verify-stage frags/sec (fd_ed25519_gpu_verify_frags, host frags)",
+            "value": args.frags / dt, "unit": "frags/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt * 1e3, "higher_is_better": True, "dtype": "u32 limbs / u8 bytes",
+            "data": "synthetic signed legacy txns (tools/synth.py), %.0f%% duplicates" % (100 * args.dup),
+            "config": {"workload": "%d frags, %d signatures, tcache depth 16 / map 64" % (args.frags, n_sigs),
+                       "arena_bytes": int(len(arena))},
+            "sigs_per_s": n_sigs / dt, "host_parse_ms": parse_ms, "results": hist, "gen_s": gen_s,
+            "cpu_baseline": None if args.no_cpu else cpu_baseline(arena, frags)}
+    print(json.dumps(line), flush=True)
+    stage.close()
+
+
+if __name__ == "__main__":
+    main()
