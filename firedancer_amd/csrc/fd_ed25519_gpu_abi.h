@@ -13,11 +13,10 @@
 #ifndef FD_VERIFY_WAVES_PER_EU
 #define FD_VERIFY_WAVES_PER_EU 2       /* -> <= 256 VGPR+AGPR per lane                */
 #endif
-#define FD_BTAB_N         129          /* [0..128]P                                   */
-#define FD_BTAB_STRIDE    32           /* u32 per entry: 3 x 10 limbs + pad           */
-#define FD_BTAB_WORDS     (2 * FD_BTAB_N * FD_BTAB_STRIDE)   /* P = B and P = 2^128 B */
-#define FD_BTAB_LOADS     ((FD_BTAB_WORDS/4 + FD_VERIFY_BLOCK - 1) / FD_VERIFY_BLOCK)   /* uint4 per thread */
-#define FD_BTAB_ALLOC     (FD_BTAB_LOADS * FD_VERIFY_BLOCK * 4)                       /* padded u32 */
+#define FD_CTAB_POS       16           /* signed 16-bit windows of w < 2^253           */
+#define FD_CTAB_N         32769        /* entries [0..2^15](2^(16 k) B) per position   */
+#define FD_CTAB_STRIDE    32           /* u32 per entry: 3 x 10 limbs + pad (128 B)    */
+#define FD_CTAB_WORDS     ((uint64_t)FD_CTAB_POS * FD_CTAB_N * FD_CTAB_STRIDE)   /* 67 MB */
 #define FD_VTAB_N         9            /* [0..8](-Q), Q = A or R                      */
 #define FD_VTAB_WORDS     40           /* u32 per entry (4 fe)                        */
 #define FD_NDIG_MAX       64           /* 4-bit windows of a <= 256-bit scalar        */
@@ -25,7 +24,7 @@
 /* LDS digit rows ([row][slot] bytes) */
 #define FD_ROW_U          0            /* signed 4-bit digits of u (sign folded in)   */
 #define FD_ROW_V          64           /* signed 4-bit digits of v                    */
-#define FD_ROW_W          128          /* signed 8-bit digits of w = v S mod l (32)   */
+#define FD_ROW_W          128          /* signed 16-bit digits of w = v S mod l: 16 x (lo, hi) rows */
 #define FD_ROW_NW         160          /* lane 0 of each wave: the wave's window count */
 #define FD_ROWS           161
 
@@ -36,7 +35,7 @@ struct verify_args {
   fd_ed25519_desc_t const * desc;
   uint64_t                  n;
   int8_t *                  out;
-  uint32_t const *          btab;      /* FD_BTAB_WORDS u32                        */
+  uint32_t const *          ctab;      /* FD_CTAB_WORDS u32: fixed-base comb table */
   uint32_t *                vtab;      /* FD_VTAB_N * FD_VTAB_WORDS * vtab_cap u32 */
   uint64_t                  vtab_cap;  /* tables                                   */
   int                       ref_codes;
@@ -45,7 +44,7 @@ struct verify_args {
 
 /* Kernel symbols in the code object (extern "C"). */
 #define FD_KERN_VERIFY   "fd_ed25519_verify_kernel"
-#define FD_KERN_BTAB     "fd_ed25519_btab_init"
+#define FD_KERN_CTAB     "fd_ed25519_ctab_init"
 #define FD_KERN_LATTEST  "fd_ed25519_lattice_test_kernel"
 #define FD_KERN_SHA512   "fd_sha512_batch_kernel"
 

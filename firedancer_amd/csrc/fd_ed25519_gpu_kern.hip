@@ -8,8 +8,10 @@
      short vector (u, v) of the lattice {u = v k mod 8l}, w = v S mod l
      (fd_lattice_dev.h) -> decode A and R (sqrt-ratio ladder), small-order
      checks -> per-lane tables [0..8](-A), [0..8](-R) in HBM ->
-     Q = [u](-A) + [v](-R) + [w]B in ONE ~130-doubling Straus chain, the B
-     part from the LDS tables of [0..128]B and [0..128]2^128 B -> Q == O.
+     Q = [u](-A) + [v](-R) in ONE ~130-doubling Straus chain, then + [w]B
+     as 16 mixed additions from the fixed-base comb table
+     [0..2^15](2^(16 k) B), k < 16 (67 MB in HBM, built once per device)
+     -> Q == O.
    Semantics follow fd_ed25519_verify (src/ballet/ed25519/fd_ed25519_user.c:
    134-229) with the FD_HAS_AVX512 error mapping (SURVEY.md §8(a) A-spec). */
 
@@ -60,32 +62,37 @@ __device__ void ge_affine_precomp( ge_precomp & q, ge_p3 & p ) {
   p.X = x; p.Y = y; fe_set1( p.Z ); p.T = xy;
 }
 
-/* Device init: thread (t, i) computes [i]P_t, P_0 = B, P_1 = 2^128 B, and
-   stores its affine precomputed form (Y+X, Y-X, 2dXY) at
-   btab[(t*FD_BTAB_N + i)*FD_BTAB_STRIDE ...].  B decoded from its standard
-   encoding (y = 4/5, x even). */
-extern "C" __global__ void fd_ed25519_btab_init( uint32_t * btab ) {
-  int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if( g >= 2*FD_BTAB_N ) return;
-  int t = g / FD_BTAB_N, i = g % FD_BTAB_N;
+/* Device init of the fixed-base comb table: thread g = k*FD_CTAB_N + j
+   computes [j](2^(16 k) B) (16 k doublings of B, then a 16-bit
+   double-and-add) and stores its affine precomputed form (Y+X, Y-X, 2dXY)
+   at ctab[g*FD_CTAB_STRIDE ...].  B decoded from its standard encoding
+   (y = 4/5, x even).  Runs once per device at context creation. */
+extern "C" __global__ void __launch_bounds__( 256 ) fd_ed25519_ctab_init( uint32_t * ctab ) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if( g >= (uint32_t)(FD_CTAB_POS*FD_CTAB_N) ) return;
+  uint32_t k = g / FD_CTAB_N, j = g % FD_CTAB_N;
   uint32_t benc[ 8 ];
   benc[0] = 0x66666658u;
 #pragma unroll
-  for( int j=1; j<8; j++ ) benc[j] = 0x66666666u;
+  for( int i=1; i<8; i++ ) benc[i] = 0x66666666u;
   ge_p3 B; ge_decode( B, benc, true );
-  if( t ) {
-    for( int j=0; j<128; j++ ) ge_dbl( B, B, true );
-  }
+#pragma unroll 1
+  for( uint32_t i=0; i<16u*k; i++ ) ge_dbl( B, B, false );
   ge_precomp Bp; ge_affine_precomp( Bp, B );
   ge_p3 acc; ge_identity( acc );
-  for( int bit=7; bit>=0; bit-- ) {
+#pragma unroll 1
+  for( int bit=15; bit>=0; bit-- ) {
     ge_dbl( acc, acc, true );
-    if( (i >> bit) & 1 ) ge_madd( acc, acc, Bp, true );
+    if( (j >> bit) & 1u ) ge_madd( acc, acc, Bp, true );
   }
   ge_precomp o; ge_affine_precomp( o, acc );
-  uint32_t * e = btab + g * FD_BTAB_STRIDE;
-  for( int j=0; j<10; j++ ) { e[j] = o.YpX.v[j]; e[10+j] = o.YmX.v[j]; e[20+j] = o.T2d.v[j]; }
-  e[30] = 0u; e[31] = 0u;
+  uint4 * e = (uint4 *)(ctab + (uint64_t)g * FD_CTAB_STRIDE);
+  uint32_t w[ 32 ];
+#pragma unroll
+  for( int i=0; i<10; i++ ) { w[i] = o.YpX.v[i]; w[10+i] = o.YmX.v[i]; w[20+i] = o.T2d.v[i]; }
+  w[30] = 0u; w[31] = 0u;
+#pragma unroll
+  for( int i=0; i<8; i++ ) e[i] = make_uint4( w[4*i], w[4*i+1], w[4*i+2], w[4*i+3] );
 }
 
 /* ------------------------------------------------------------------ verify */
@@ -224,13 +231,17 @@ __device__ __forceinline__ void vtab_finish( ge_cached & c, uint32_t const w[ 40
   }
 }
 
-__device__ __forceinline__ void btab_load( ge_precomp & q, uint32_t const * lds_btab, uint32_t db ) {
-  bool neg = db < 128u;
-  uint32_t e = neg ? 128u - db : db - 128u;
-  uint4 const * p = (uint4 const *)(lds_btab + e * FD_BTAB_STRIDE);
-  uint32_t w[ 32 ];
+/* Comb-table entry |d| of position k (signed 16-bit digit d): loads issued
+   here, sign applied by ctab_finish at the use point. */
+__device__ __forceinline__ void ctab_fetch( uint32_t w[ 32 ], uint32_t const * ctab, int k, int d ) {
+  uint32_t e = (uint32_t)(d < 0 ? -d : d);
+  uint4 const * p = (uint4 const *)(ctab + ((uint64_t)k * FD_CTAB_N + e) * FD_CTAB_STRIDE);
 #pragma unroll
   for( int j=0; j<8; j++ ) { uint4 v = p[j]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
+}
+
+__device__ __forceinline__ void ctab_finish( ge_precomp & q, uint32_t const w[ 32 ], int d ) {
+  bool neg = d < 0;
   fe t, tn;
 #pragma unroll
   for( int j=0; j<10; j++ ) t.v[j] = w[20+j];
@@ -243,24 +254,35 @@ __device__ __forceinline__ void btab_load( ge_precomp & q, uint32_t const * lds_
   }
 }
 
-/* acc = [u](-A) + [v](-R) + [w_lo]B + [w_hi](2^128 B) over nw 4-bit windows
-   (wave-uniform; one shared doubling chain -- Straus).  u / v digits from
-   LDS rows (biased by 8, sign of u folded in), w digits (biased by 128)
-   at every other window.  Table entries are fetched one step ahead: A's for
-   the next window before the doublings, R's before A's addition. */
+__device__ __forceinline__ int wdig( uint8_t const * dig, int k ) {
+  uint32_t lo = dig[ (FD_ROW_W + 2*k)*FD_VERIFY_BLOCK ], hi = dig[ (FD_ROW_W + 2*k + 1)*FD_VERIFY_BLOCK ];
+  return (int)(int16_t)(uint16_t)(lo | (hi << 8));
+}
+
+/* acc = [u](-A) + [v](-R) over nw 4-bit windows (wave-uniform; one shared
+   doubling chain -- Straus), then + [w]B as 16 mixed additions of comb-table
+   entries (no doublings: entry k already carries its 2^(16 k)).  u / v
+   digits from LDS rows (biased by 8, sign of u folded in), w digits signed
+   16-bit.  Table entries are fetched one step ahead: A's for the next window
+   before the doublings, R's before A's addition, the first comb entry during
+   the last window. */
 __device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, uint64_t cap, uint64_t ta, uint64_t tr,
-                                          uint8_t const * dig, uint32_t const * lds_bt, int nw ) {
+                                          uint8_t const * dig, uint32_t const * ctab, int nw ) {
   ge_identity( acc );
   uint32_t raw[ 40 ];
+  uint32_t craw[ 32 ];
   uint32_t dba = dig[ (FD_ROW_U + nw-1)*FD_VERIFY_BLOCK ];
   vtab_fetch( raw, vtab, cap, ta, dba );
 #pragma unroll 1
   for( int i=nw-1; i>=0; i-- ) {
     if( i < nw-1 ) {
+      /* T only on the last doubling (the adds need it); a runtime want_t in
+         a rolled loop would compute it on all four */
 #pragma unroll 1
-      for( int j=0; j<4; j++ ) { ge_dbl( acc, acc, j == 3 ); FE_FENCE(); }
+      for( int j=0; j<3; j++ ) { ge_dbl( acc, acc, false ); FE_FENCE(); }
+      ge_dbl( acc, acc, true );
+      FE_FENCE();
     }
-    bool bq = ((i & 1) == 0) && (i <= 30);
     ge_cached q;
     vtab_finish( q, raw, dba );
     uint32_t dbr = dig[ (FD_ROW_V + i)*FD_VERIFY_BLOCK ];
@@ -270,20 +292,19 @@ __device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, ui
     FE_FENCE();
     vtab_finish( q, raw, dbr );
     if( i > 0 ) { dba = dig[ (FD_ROW_U + i-1)*FD_VERIFY_BLOCK ]; vtab_fetch( raw, vtab, cap, ta, dba ); }
+    else        ctab_fetch( craw, ctab, 0, wdig( dig, 0 ) );
     FE_FENCE();
-    ge_add_cached( acc, acc, q, bq );
+    ge_add_cached( acc, acc, q, i == 0 );
     FE_FENCE();
-    if( bq ) {
-      ge_precomp bp;
-      btab_load( bp, lds_bt, dig[ (FD_ROW_W + (i>>1))*FD_VERIFY_BLOCK ] );
-      FE_FENCE();
-      ge_madd( acc, acc, bp, true );
-      FE_FENCE();
-      btab_load( bp, lds_bt + FD_BTAB_N*FD_BTAB_STRIDE, dig[ (FD_ROW_W + 16 + (i>>1))*FD_VERIFY_BLOCK ] );
-      FE_FENCE();
-      ge_madd( acc, acc, bp, false );
-      FE_FENCE();
-    }
+  }
+#pragma unroll 1
+  for( int k=0; k<FD_CTAB_POS; k++ ) {
+    ge_precomp bp;
+    ctab_finish( bp, craw, wdig( dig, k ) );
+    if( k + 1 < FD_CTAB_POS ) ctab_fetch( craw, ctab, k + 1, wdig( dig, k + 1 ) );
+    FE_FENCE();
+    ge_madd( acc, acc, bp, k + 1 < FD_CTAB_POS );
+    FE_FENCE();
   }
 }
 
@@ -319,7 +340,6 @@ __device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 
    decode R, small-order A, small-order R, equation. */
 extern "C" __global__ void __launch_bounds__( FD_VERIFY_BLOCK, FD_VERIFY_WAVES_PER_EU )
 fd_ed25519_verify_kernel( verify_args args ) {
-  __shared__ uint4    s_btab4[ FD_BTAB_WORDS / 4 ];
   __shared__ uint8_t  s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
 
   int tid = (int)threadIdx.x;
@@ -329,11 +349,9 @@ fd_ed25519_verify_kernel( verify_args args ) {
   STAMP( 0 );
   uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)tid;
   uint64_t cap = args.vtab_cap;
-  uint32_t const * s_btab = (uint32_t const *)s_btab4;
   /* Every lane stays to the wave-wide window count below (no early exit):
      lanes past n or with a bad descriptor take the no-work path.  The
-     descriptor / signature / key loads are issued before the B-table copy
-     so their latency overlaps it. */
+     descriptor / signature / key loads are issued first. */
   bool valid = gid < args.n;
   fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
   if( valid ) d = args.desc[ gid ];
@@ -351,21 +369,6 @@ fd_ed25519_verify_kernel( verify_args args ) {
     load_words<16>( sig, args.arena, d.sig_off, lim_dw );
     load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
   }
-
-  {
-    /* all of this thread's table loads in flight at once (the device copy is
-       padded to FD_BTAB_LOADS full rounds), then the LDS stores */
-    uint4 const * g = (uint4 const *)args.btab;
-    uint4 t[ FD_BTAB_LOADS ];
-#pragma unroll
-    for( int r=0; r<FD_BTAB_LOADS; r++ ) t[r] = g[ tid + r*FD_VERIFY_BLOCK ];
-#pragma unroll
-    for( int r=0; r<FD_BTAB_LOADS; r++ ) {
-      int i = tid + r*FD_VERIFY_BLOCK;
-      if( r < FD_BTAB_LOADS-1 || i < FD_BTAB_WORDS/4 ) s_btab4[i] = t[r];
-    }
-  }
-  __syncthreads();
   STAMP( 1 );
 
   bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                           /* :157-159 */
@@ -397,10 +400,17 @@ fd_ed25519_verify_kernel( verify_args args ) {
       }
       uint32_t w[ 8 ];
       sc_reduce512( w, pr );
-      uint8_t ds[ 32 ];
-      sc_recode_w8( ds, w );
+      /* signed 16-bit windows: d_k in [-2^15, 2^15), the top one (w < 2^253)
+         keeps its carry: d_15 <= 2^13 */
+      int c = 0;
 #pragma unroll
-      for( int i=0; i<32; i++ ) drow[ (FD_ROW_W + i)*FD_VERIFY_BLOCK ] = ds[i];
+      for( int k=0; k<FD_CTAB_POS; k++ ) {
+        int dd = (int)((w[k>>1] >> (16*(k&1))) & 0xffffu) + c;
+        c = dd >= 32768 && k < FD_CTAB_POS-1;
+        dd -= c << 16;
+        drow[ (FD_ROW_W + 2*k    )*FD_VERIFY_BLOCK ] = (uint8_t)(dd & 255);
+        drow[ (FD_ROW_W + 2*k + 1)*FD_VERIFY_BLOCK ] = (uint8_t)((dd >> 8) & 255);
+      }
       nbits = max( bitlen8( u ), bitlen8( v ) );
     }
     /* wave-uniform window count: x < 2^(4 nw - 1) for every lane's u, v */
@@ -448,7 +458,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
   if( code == 0 ) {
     int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
     ge_p3 acc;
-    dsm_loop( acc, args.vtab, cap, gid, cap/2u + gid, drow, s_btab, nw );
+    dsm_loop( acc, args.vtab, cap, gid, cap/2u + gid, drow, args.ctab, nw );
     STAMP( 5 );
     /* Q == O  <=>  X == 0 and Y == Z (the reference's projective compare, :225-228, on [v]D) */
     fe dl;
