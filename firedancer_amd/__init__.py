@@ -20,3 +20,4 @@ from .verify_stage import (  # noqa: F401
     FD_TXN_VERIFY_BAD_FRAG, FD_TXN_VERIFY_DEDUP, FD_TXN_VERIFY_FAILED, FD_TXN_VERIFY_SUCCESS, FRAG_DTYPE, TCache,
     VerifyStage, frags_to_descs,
 )
+from .offload import OffloadLink, ServeThread, load_offload_lib, server_path  # noqa: F401

@@ -1,0 +1,59 @@
+/* fd_verify_offload_server -- the GPU offload process of include/fd_verify_offload.h.
+
+     fd_verify_offload_server [--name /fd_verify_offload] [--depth 262144]
+                              [--dcache-mb 512] [--batch 65536] [--threads 4]
+                              [--gpus 0x1] [--tcache-depth 16] [--tcache-map 64]
+
+   Creates the shared-memory link, owns the GPU context and the verify tile's
+   ha-dedup tcache (default depth 16 / map 64, fd_verify.h:6-7), serves until
+   a client calls fd_verify_offload_halt (or SIGINT / SIGTERM), prints one
+   JSON line of stats and removes the link. */
+
+#include "../../include/fd_ed25519_gpu.h"
+#include "../../include/fd_verify_offload.h"
+
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static fd_verify_offload_t * g_off;
+static void on_signal( int sig ) { (void)sig; if( g_off ) fd_verify_offload_halt( g_off ); }
+
+int main( int argc, char ** argv ) {
+  char const * name = "/fd_verify_offload";
+  uint64_t depth = 1ull << 18, dcache_mb = 512, batch = 65536, gpus = 1, tdepth = 16, tmap = 64;
+  int threads = 4;
+  for( int i=1; i+1<argc; i+=2 ) {
+    if     ( !strcmp( argv[i], "--name"         ) ) name      = argv[i+1];
+    else if( !strcmp( argv[i], "--depth"        ) ) depth     = strtoull( argv[i+1], NULL, 0 );
+    else if( !strcmp( argv[i], "--dcache-mb"    ) ) dcache_mb = strtoull( argv[i+1], NULL, 0 );
+    else if( !strcmp( argv[i], "--batch"        ) ) batch     = strtoull( argv[i+1], NULL, 0 );
+    else if( !strcmp( argv[i], "--threads"      ) ) threads   = atoi( argv[i+1] );
+    else if( !strcmp( argv[i], "--gpus"         ) ) gpus      = strtoull( argv[i+1], NULL, 0 );
+    else if( !strcmp( argv[i], "--tcache-depth" ) ) tdepth    = strtoull( argv[i+1], NULL, 0 );
+    else if( !strcmp( argv[i], "--tcache-map"   ) ) tmap      = strtoull( argv[i+1], NULL, 0 );
+    else { fprintf( stderr, "unknown option %s\n", argv[i] ); return 2; }
+  }
+  fd_verify_offload_t * off = fd_verify_offload_create( name, depth, dcache_mb << 20 );
+  if( !off ) { fprintf( stderr, "fd_verify_offload_create(%s) failed\n", name ); return 1; }
+  g_off = off;
+  signal( SIGINT, on_signal ); signal( SIGTERM, on_signal );
+  fd_ed25519_gpu_t * ctx = fd_ed25519_gpu_new( gpus, batch * 4u );   /* larger batches are chunked internally */
+  fd_ed25519_gpu_tcache_t * tc = fd_ed25519_gpu_tcache_new( tdepth, tmap );
+  if( !ctx || !tc ) { fprintf( stderr, "GPU context / tcache creation failed\n" ); fd_verify_offload_unlink( name ); return 1; }
+  fprintf( stderr, "fd_verify_offload_server: serving %s (depth %lu, frag area %lu MB, batch %lu)\n",
+           name, (unsigned long)depth, (unsigned long)dcache_mb, (unsigned long)batch );
+  fflush( stderr );
+  /* readiness marker for scripts: the link exists and the GPU is up */
+  printf( "{\"ready\": true}\n" ); fflush( stdout );
+  uint64_t stats[ 4 ] = { 0, 0, 0, 0 };
+  int err = fd_verify_offload_serve( off, ctx, tc, batch, threads, stats );
+  printf( "{\"err\": %d, \"batches\": %lu, \"frags\": %lu, \"max_batch\": %lu, \"idle_polls\": %lu}\n", err,
+          (unsigned long)stats[0], (unsigned long)stats[1], (unsigned long)stats[2], (unsigned long)stats[3] );
+  fd_ed25519_gpu_tcache_delete( tc );
+  fd_ed25519_gpu_delete( ctx );
+  fd_verify_offload_leave( off );
+  fd_verify_offload_unlink( name );
+  return err ? 1 : 0;
+}

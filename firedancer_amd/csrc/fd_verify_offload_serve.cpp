@@ -1,0 +1,70 @@
+/* fd_verify_offload_serve.cpp -- the GPU side of include/fd_verify_offload.h:
+   drains the frag ring in seq order through the asynchronous verify stage
+   (fd_ed25519_gpu_stage_*, fd_verify_stage.cpp) and publishes per-frag
+   results in seq order.
+
+   Batching policy: a batch is cut at the ring end and at a frag-area wrap
+   (so its bytes are one contiguous span for the copy to HBM) and holds at
+   most max_batch frags.  With the GPU idle any available frags go at once;
+   with one batch outstanding the next is submitted when at least
+   max_batch/2 frags wait, or when the outstanding batch has completed --
+   so under load batches grow to max_batch and the host parse of one batch
+   overlaps the GPU work of the previous one (two in flight), and at low
+   load latency stays at one batch. */
+
+#include "../../include/fd_ed25519_gpu.h"
+#include "../../include/fd_verify_offload.h"
+
+#include <time.h>
+
+extern "C" int
+fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,
+                         uint64_t max_batch, int threads, uint64_t * stats /* [4]: batches, frags, max batch, idle polls */ ) {
+  if( !off || !ctx || !tc || !max_batch ) return FD_ED25519_GPU_ERR_ARG;
+  fd_ed25519_gpu_stage_t * st = fd_ed25519_gpu_stage_new( ctx, tc, max_batch, threads );
+  if( !st ) return FD_ED25519_GPU_ERR_OOM;
+  uint64_t q_seq[ 2 ], q_cnt[ 2 ];   /* outstanding batches, oldest first */
+  int q = 0;
+  uint64_t done = fd_verify_offload_done_seq( off );
+  uint64_t s_batches = 0, s_frags = 0, s_max = 0, s_idle = 0;
+  int err = FD_ED25519_GPU_OK;
+  uint8_t * dc = fd_verify_offload_dcache( off );
+  uint64_t dsz = fd_verify_offload_dcache_sz( off );
+  for(;;) {
+    int progressed = 0;
+    uint64_t first, avail = fd_verify_offload_avail( off, &first );
+    if( q < 2 && avail && (q == 0 || avail >= max_batch/2u) ) {
+      uint64_t m = avail < max_batch ? avail : max_batch;
+      fd_verify_offload_frag_t const * f = fd_verify_offload_frag_laddr( off, first );
+      for( uint64_t j=1; j<m; j++ ) if( f[ j ].off < f[ j-1 ].off ) { m = j; break; }   /* frag-area wrap */
+      err = fd_ed25519_gpu_stage_submit( st, dc, dsz, (fd_ed25519_gpu_frag_t const *)f, m,
+                                         fd_verify_offload_result_laddr( off, first ),
+                                         fd_verify_offload_sig_laddr( off, first ) );
+      if( err ) break;
+      fd_verify_offload_take( off, m );
+      q_seq[ q ] = first; q_cnt[ q ] = m; q++;
+      s_batches++; s_frags += m; s_max = m > s_max ? m : s_max;
+      progressed = 1;
+    }
+    if( q ) {
+      /* block on the GPU only when there is nothing else to do */
+      uint64_t f2; int more = fd_verify_offload_avail( off, &f2 ) != 0;
+      int r = fd_ed25519_gpu_stage_poll( st, !progressed && !more );
+      if( r == FD_ED25519_GPU_OK ) {
+        done = q_seq[ 0 ] + q_cnt[ 0 ];
+        fd_verify_offload_complete( off, done );
+        q_seq[ 0 ] = q_seq[ 1 ]; q_cnt[ 0 ] = q_cnt[ 1 ]; q--;
+        progressed = 1;
+      } else if( r != FD_ED25519_GPU_PENDING ) { err = r; break; }
+    }
+    if( !progressed ) {
+      if( fd_verify_offload_halted( off ) && !q && !fd_verify_offload_avail( off, NULL ) ) break;
+      s_idle++;
+      struct timespec ts = { 0, 20000 };   /* 20 us */
+      nanosleep( &ts, NULL );
+    }
+  }
+  fd_ed25519_gpu_stage_delete( st );
+  if( stats ) { stats[0] = s_batches; stats[1] = s_frags; stats[2] = s_max; stats[3] = s_idle; }
+  return err;
+}

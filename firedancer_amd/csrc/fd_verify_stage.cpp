@@ -32,6 +32,8 @@
 
 #include <stdlib.h>
 #include <string.h>
+#include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/fd_ed25519_gpu.h"
@@ -240,50 +242,230 @@ fd_ed25519_gpu_frags_to_descs( uint8_t const * arena, uint64_t arena_sz,
 
 /* ---- the whole stage ---------------------------------------------------- */
 
-extern "C" int
-fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,
-                             uint8_t const * arena, uint64_t arena_sz,
-                             fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt,
-                             int8_t * result, uint64_t * sig_out ) {
-  if( !ctx || !tc || !result || !sig_out || (!frag && frag_cnt) ) return FD_ED25519_GPU_ERR_ARG;
-  if( !frag_cnt ) return FD_ED25519_GPU_OK;
-  std::vector<fd_ed25519_desc_t> desc( 16u * frag_cnt );
-  std::vector<uint64_t> tag( frag_cnt );
-  std::vector<uint8_t>  cnts( frag_cnt );
-  if( !arena && arena_sz ) return FD_ED25519_GPU_ERR_ARG;
-  int64_t n = frags_collect( arena, arena_sz, frag, frag_cnt, desc.data(), desc.size(), result, tag.data(),
-                             cnts.data() );
-  if( n < 0 ) return (int)n;
-  std::vector<int8_t> code( n > 0 ? (size_t)n : 1u );
-  if( n > 0 ) {
-    int err = fd_ed25519_verify_batch_gpu( ctx, arena, arena_sz, desc.data(), (uint64_t)n, code.data() );
-    if( err ) return err;
+/* One batch of frags between parse and replay. */
+struct vs_batch {
+  int                            state;     /* 0 free, 1 parsed, 2 on the GPU, 3 GPU done / nothing to verify */
+  uint8_t const *                arena;     /* rebased: the span the descriptors touch */
+  uint64_t                       arena_sz;
+  uint64_t                       n;         /* frags */
+  int64_t                        ndesc;
+  int8_t *                       result;    /* caller's, n */
+  uint64_t *                     sig;       /* caller's, n */
+  std::vector<fd_ed25519_desc_t> desc;
+  std::vector<uint64_t>          tag;
+  std::vector<uint8_t>           cnt;
+  std::vector<int8_t>            code;
+  std::vector<uint32_t>          fld;       /* per frag: sig_off, pub_off, msg_off, msg_sz (parallel parse) */
+};
+
+struct fd_ed25519_gpu_stage {
+  fd_ed25519_gpu_t *        ctx;
+  fd_ed25519_gpu_tcache_t * tc;
+  uint64_t                  max_frags;
+  int                       threads;
+  int                       head;          /* oldest pending slot */
+  int                       pending;       /* 0..2 */
+  vs_batch                  b[ 2 ];
+};
+
+/* Parse frags [lo, hi) of a batch into per-frag status / tag / count / fields. */
+static void
+vs_parse_range( vs_batch * b, uint8_t const * arena, uint64_t arena_sz, fd_ed25519_gpu_frag_t const * frag,
+                uint64_t lo, uint64_t hi ) {
+  for( uint64_t i=lo; i<hi; i++ ) {
+    uint32_t so = 0, po = 0, mo = 0, ms = 0, cnt = 0;
+    int st = frag_parse( arena, arena_sz, frag[ i ], &b->tag[ i ], &so, &po, &mo, &ms, &cnt );
+    b->result[ i ] = (int8_t)st;
+    b->cnt[ i ] = (uint8_t)(st ? 0u : cnt);
+    uint32_t * f = &b->fld[ 4u*i ];
+    f[0] = so; f[1] = po; f[2] = mo; f[3] = ms;
   }
-  /* In-order replay of fd_txn_verify's tcache steps (fd_verify.h:63-86). */
+}
+
+/* Descriptors of frags [lo, hi) starting at descriptor index at. */
+static void
+vs_emit_range( vs_batch * b, uint64_t lo, uint64_t hi, uint64_t at ) {
+  for( uint64_t i=lo; i<hi; i++ ) {
+    uint32_t const * f = &b->fld[ 4u*i ];
+    for( uint32_t j=0; j<b->cnt[ i ]; j++ ) {
+      fd_ed25519_desc_t * d = &b->desc[ at++ ];
+      d->sig_off = f[0] + 64u*j; d->pub_off = f[1] + 32u*j; d->msg_off = f[2];
+      d->msg_sz = (uint16_t)f[3]; d->txn_idx = (uint16_t)i;
+    }
+  }
+}
+
+/* Host step 1 for a whole batch, on up to `threads` host threads (two passes:
+   per-frag parse, then descriptors at prefix-summed positions), then the
+   descriptors are rebased onto the arena span they touch so only that span is
+   copied to the GPU. */
+static void
+vs_parse( vs_batch * b, uint8_t const * arena, uint64_t arena_sz, fd_ed25519_gpu_frag_t const * frag, uint64_t n,
+          int threads ) {
+  b->n = n;
+  b->tag.resize( n ); b->cnt.resize( n ); b->fld.resize( 4u*n );
+  int nt = (n >= 8192u && threads > 1) ? threads : 1;
+  std::vector<uint64_t> part( (size_t)nt + 1u );
+  for( int t=0; t<=nt; t++ ) part[ t ] = n * (uint64_t)t / (uint64_t)nt;
+  std::vector<uint64_t> base( (size_t)nt + 1u, 0u );
+  if( nt == 1 ) vs_parse_range( b, arena, arena_sz, frag, 0u, n );
+  else {
+    std::vector<std::thread> th;
+    for( int t=0; t<nt; t++ ) th.emplace_back( vs_parse_range, b, arena, arena_sz, frag, part[t], part[t+1] );
+    for( auto & x : th ) x.join();
+  }
+  for( int t=0; t<nt; t++ ) {
+    uint64_t c = 0;
+    for( uint64_t i=part[t]; i<part[t+1]; i++ ) c += b->cnt[ i ];
+    base[ t+1 ] = base[ t ] + c;
+  }
+  b->ndesc = (int64_t)base[ nt ];
+  b->desc.resize( b->ndesc ? (size_t)b->ndesc : 1u );
+  if( nt == 1 ) vs_emit_range( b, 0u, n, 0u );
+  else {
+    std::vector<std::thread> th;
+    for( int t=0; t<nt; t++ ) th.emplace_back( vs_emit_range, b, part[t], part[t+1], base[t] );
+    for( auto & x : th ) x.join();
+  }
+  /* rebase onto [lo, hi) */
+  uint64_t lo = ~0ull, hi = 0u;
+  for( int64_t k=0; k<b->ndesc; k++ ) {
+    fd_ed25519_desc_t const * d = &b->desc[ k ];
+    uint64_t a0 = d->sig_off < d->pub_off ? d->sig_off : d->pub_off; a0 = a0 < d->msg_off ? a0 : d->msg_off;
+    uint64_t e0 = (uint64_t)d->sig_off + 64u, e1 = (uint64_t)d->pub_off + 32u, e2 = (uint64_t)d->msg_off + d->msg_sz;
+    uint64_t e = e0 > e1 ? e0 : e1; e = e > e2 ? e : e2;
+    lo = a0 < lo ? a0 : lo; hi = e > hi ? e : hi;
+  }
+  if( b->ndesc ) {
+    for( int64_t k=0; k<b->ndesc; k++ ) {
+      fd_ed25519_desc_t * d = &b->desc[ k ];
+      d->sig_off -= (uint32_t)lo; d->pub_off -= (uint32_t)lo; d->msg_off -= (uint32_t)lo;
+    }
+    b->arena = arena + lo; b->arena_sz = hi - lo;
+  } else {
+    b->arena = arena; b->arena_sz = 0u;
+  }
+  b->code.resize( b->ndesc ? (size_t)b->ndesc : 1u );
+}
+
+/* In-order replay of fd_txn_verify's tcache steps (fd_verify.h:63-86) over a
+   batch whose GPU codes are in. */
+static void
+vs_replay( fd_ed25519_gpu_tcache_t * tc, vs_batch * b ) {
   uint64_t k = 0;
-  for( uint64_t i=0; i<frag_cnt; i++ ) {
-    sig_out[ i ] = 0u;
-    int st = result[ i ];
+  for( uint64_t i=0; i<b->n; i++ ) {
+    b->sig[ i ] = 0u;
+    int st = b->result[ i ];
     if( st == FD_TXN_VERIFY_BAD_FRAG ) continue;
     int8_t vcode = FD_ED25519_ERR_SIG;
     if( !st ) {
       /* fold this frag's codes with fd_ed25519_verify_batch_single_msg's
          precedence (first phase-1 error, else ERR_MSG, else SUCCESS) */
-      uint64_t cnt = cnts[ i ];
+      uint64_t cnt = b->cnt[ i ];
       int8_t first = 0, any_msg = 0;
       for( uint64_t j=0; j<cnt; j++ ) {
-        int8_t c = code[ k + j ];
+        int8_t c = b->code[ k + j ];
         if( c == FD_ED25519_ERR_MSG ) any_msg = 1;
         else if( c != FD_ED25519_SUCCESS && !first ) first = c;
       }
       vcode = first ? first : (any_msg ? (int8_t)FD_ED25519_ERR_MSG : (int8_t)FD_ED25519_SUCCESS);
       k += cnt;
     }
-    if( fd_ed25519_gpu_tcache_query( tc, tag[ i ] ) ) { result[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
-    if( vcode != FD_ED25519_SUCCESS )                 { result[ i ] = FD_TXN_VERIFY_FAILED; continue; }
-    if( tc_insert( tc, tag[ i ] ) )                   { result[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
-    result[ i ] = FD_TXN_VERIFY_SUCCESS;
-    sig_out[ i ] = tag[ i ];
+    uint64_t tag = b->tag[ i ];
+    if( fd_ed25519_gpu_tcache_query( tc, tag ) ) { b->result[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
+    if( vcode != FD_ED25519_SUCCESS )            { b->result[ i ] = FD_TXN_VERIFY_FAILED; continue; }
+    if( tc_insert( tc, tag ) )                   { b->result[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
+    b->result[ i ] = FD_TXN_VERIFY_SUCCESS;
+    b->sig[ i ] = tag;
   }
+}
+
+static int
+vs_launch( fd_ed25519_gpu_t * ctx, vs_batch * b ) {
+  if( !b->ndesc ) { b->state = 3; return FD_ED25519_GPU_OK; }
+  int err = fd_ed25519_gpu_submit( ctx, b->arena, b->arena_sz, b->desc.data(), (uint64_t)b->ndesc, b->code.data() );
+  if( err ) return err;
+  b->state = 2;
+  return FD_ED25519_GPU_OK;
+}
+
+extern "C" fd_ed25519_gpu_stage_t *
+fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, uint64_t max_frags, int threads ) {
+  if( !ctx || !tc || !max_frags ) return NULL;
+  fd_ed25519_gpu_stage_t * st = new (std::nothrow) fd_ed25519_gpu_stage_t();
+  if( !st ) return NULL;
+  st->ctx = ctx; st->tc = tc; st->max_frags = max_frags;
+  st->threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+  return st;
+}
+
+extern "C" void
+fd_ed25519_gpu_stage_delete( fd_ed25519_gpu_stage_t * st ) {
+  if( !st ) return;
+  while( st->pending ) if( fd_ed25519_gpu_stage_poll( st, 1 ) < 0 ) break;
+  delete st;
+}
+
+extern "C" int
+fd_ed25519_gpu_stage_submit( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, uint64_t arena_sz,
+                             fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt, int8_t * result, uint64_t * sig ) {
+  if( !st || (!frag && frag_cnt) || (frag_cnt && (!result || !sig)) || (!arena && arena_sz) ) return FD_ED25519_GPU_ERR_ARG;
+  if( frag_cnt > st->max_frags ) return FD_ED25519_GPU_ERR_ARG;
+  if( st->pending == 2 ) return FD_ED25519_GPU_ERR_BUSY;
+  vs_batch * b = &st->b[ (st->head + st->pending) & 1 ];
+  b->result = result; b->sig = sig;
+  vs_parse( b, arena, arena_sz, frag, frag_cnt, st->threads );
+  b->state = 1;
+  st->pending++;
+  if( st->pending == 1 ) return vs_launch( st->ctx, b );   /* the GPU is free: go */
+  return FD_ED25519_GPU_OK;                                  /* launched when the older batch's GPU work ends */
+}
+
+extern "C" int
+fd_ed25519_gpu_stage_poll( fd_ed25519_gpu_stage_t * st, int block ) {
+  if( !st ) return FD_ED25519_GPU_ERR_ARG;
+  if( !st->pending ) return FD_ED25519_GPU_OK;
+  vs_batch * b = &st->b[ st->head ];
+  if( b->state == 1 ) { int err = vs_launch( st->ctx, b ); if( err ) return err; }
+  if( b->state == 2 ) {
+    for(;;) {
+      int r = fd_ed25519_gpu_poll( st->ctx );
+      if( r == FD_ED25519_GPU_OK ) break;
+      if( r != FD_ED25519_GPU_PENDING ) { b->state = 0; st->pending--; st->head ^= 1; return r; }
+      if( !block ) return FD_ED25519_GPU_PENDING;
+      std::this_thread::yield();
+    }
+    b->state = 3;
+  }
+  /* the GPU is free: start the next batch before the host replays this one */
+  if( st->pending == 2 ) {
+    vs_batch * nb = &st->b[ st->head ^ 1 ];
+    if( nb->state == 1 ) { int err = vs_launch( st->ctx, nb ); if( err ) return err; }
+  }
+  vs_replay( st->tc, b );
+  b->state = 0;
+  st->pending--;
+  st->head ^= 1;
+  return FD_ED25519_GPU_OK;
+}
+
+extern "C" int
+fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st ) { return st ? st->pending : 0; }
+
+extern "C" int
+fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,
+                             uint8_t const * arena, uint64_t arena_sz,
+                             fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt,
+                             int8_t * result, uint64_t * sig_out ) {
+  if( !ctx || !tc || (frag_cnt && (!result || !sig_out || !frag)) || (!arena && arena_sz) ) return FD_ED25519_GPU_ERR_ARG;
+  if( !frag_cnt ) return FD_ED25519_GPU_OK;
+  vs_batch b;
+  b.result = result; b.sig = sig_out;
+  vs_parse( &b, arena, arena_sz, frag, frag_cnt, 1 );
+  if( b.ndesc ) {
+    int err = fd_ed25519_verify_batch_gpu( ctx, b.arena, b.arena_sz, b.desc.data(), (uint64_t)b.ndesc, b.code.data() );
+    if( err ) return err;
+  }
+  vs_replay( tc, &b );
   return FD_ED25519_GPU_OK;
 }

@@ -215,6 +215,30 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
                                  fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt,
                                  int8_t * result, uint64_t * sig_out );
 
+/* Asynchronous, double-buffered form of the stage (the batching verify tile
+   of SURVEY.md §8(f) next-1): submit parses a batch of frags on the host (on
+   up to `threads` host threads) and hands it to the GPU if the GPU is free;
+   poll completes the OLDEST outstanding batch -- when its GPU work is done it
+   starts the next batch's GPU work, then replays the tcache steps for the
+   completed batch and fills its result / sig arrays -- and returns
+   FD_ED25519_GPU_OK, or FD_ED25519_GPU_PENDING (block == 0 only).  At most two
+   batches are outstanding (submit returns FD_ED25519_GPU_ERR_BUSY on a
+   third), so the host parse of batch k+1 and the replay of batch k overlap
+   the GPU.  Batches complete strictly in submission order, which keeps the
+   tile's frag order for the tcache.  The frag bytes and the result / sig
+   arrays of a batch must stay valid until its poll returns OK.  The stage
+   uses ctx's async pair: no other submit on ctx while batches are pending. */
+typedef struct fd_ed25519_gpu_stage fd_ed25519_gpu_stage_t;
+
+fd_ed25519_gpu_stage_t * fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,
+                                                   uint64_t max_frags, int threads );
+void fd_ed25519_gpu_stage_delete ( fd_ed25519_gpu_stage_t * st );   /* completes outstanding batches */
+int  fd_ed25519_gpu_stage_submit ( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, uint64_t arena_sz,
+                                   fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt,
+                                   int8_t * result, uint64_t * sig );
+int  fd_ed25519_gpu_stage_poll   ( fd_ed25519_gpu_stage_t * st, int block );
+int  fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st );
+
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
    u32 words each, k < l) on the context's first device.  out: n records of

@@ -19,10 +19,15 @@ def lib():
     return fa.load_lib()
 
 
-def declared_functions():
-    src = open(HDR).read()
+def declared_functions(path=HDR, prefix="fd_"):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(fd_ed25519_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(%s\w+)\s*\(" % prefix, src)))
+
+
+def exported(path):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path]).decode()
+    return set(l.split()[-1] for l in out.splitlines() if " T " in l)
 
 
 def test_header_declares_the_boundary():
@@ -36,12 +41,26 @@ def test_header_declares_the_boundary():
 
 def test_library_exports_every_declared_symbol(lib):
     import firedancer_amd as fa
-    out = subprocess.check_output(["nm", "-D", "--defined-only", fa.lib_path()]).decode()
-    exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
-    missing = [f for f in declared_functions() if f not in exported]
+    missing = [f for f in declared_functions() if f not in exported(fa.lib_path())]
     assert not missing, missing
     for f in declared_functions():
         getattr(lib, f)
+
+
+def test_offload_headers_and_libraries():
+    """include/fd_verify_offload.h: the client/link functions live in the
+    HIP-free libfd_verify_offload.so (a sandboxed tile links only that), the
+    server loop in libfd_ed25519_gpu.so; the server executable is built."""
+    import firedancer_amd as fa
+    fa.load_offload_lib()
+    decl = declared_functions(os.path.join(REPO, "include", "fd_verify_offload.h"))
+    link = exported(fa.offload.offload_lib_path())
+    gpu = exported(fa.lib_path())
+    assert [f for f in decl if f != "fd_verify_offload_serve" and f not in link] == []
+    assert "fd_verify_offload_serve" in gpu
+    needed = subprocess.check_output(["readelf", "-d", fa.offload.offload_lib_path()]).decode()
+    assert "amdhip64" not in needed
+    assert os.access(fa.server_path(), os.X_OK)
 
 
 def test_strerror_matches_reference_strings(lib):

@@ -317,3 +317,105 @@ def test_verify_frags_random_stream_vs_reference_tile(gpu, ref):
     assert len(bad) == 0, [(int(j), int(got_res[j]), int(exp_res[j])) for j in bad[:10]]
     hist = {int(k): int(v) for k, v in zip(*np.unique(exp_res, return_counts=True))}
     assert hist.get(S, 0) > 1000 and hist.get(D, 0) > 300 and hist.get(F, 0) > 300 and hist.get(BAD, 0) > 30, hist
+
+
+@pytest.mark.gpu
+def test_stage_async_two_in_flight_vs_reference_tile(gpu, ref):
+    """The asynchronous stage (fd_ed25519_gpu_stage_*): batches of varying
+    size submitted with up to two outstanding, completed in order; results
+    equal the sequential reference tile's."""
+    import ctypes as C
+    rng = np.random.default_rng(77)
+    arena, frags = _random_frag_stream(rng, 1500, 4000)
+    exp_res, exp_tag = ref_seq(ref, arena, frags)
+    lib = fa.load_lib()
+    vp = C.c_void_p
+    lib.fd_ed25519_gpu_stage_new.restype = vp
+    lib.fd_ed25519_gpu_stage_new.argtypes = [vp, vp, C.c_uint64, C.c_int]
+    lib.fd_ed25519_gpu_stage_submit.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp]
+    lib.fd_ed25519_gpu_stage_poll.argtypes = [vp, C.c_int]
+    lib.fd_ed25519_gpu_stage_pending.argtypes = [vp]
+    lib.fd_ed25519_gpu_stage_delete.argtypes = [vp]
+    tc = fa.TCache()
+    st = lib.fd_ed25519_gpu_stage_new(gpu.ctx, tc.tc, 4096, 4)
+    assert st
+    res = np.zeros(len(frags), np.int8)
+    sig = np.zeros(len(frags), np.uint64)
+    fr = np.ascontiguousarray(frags)
+    bounds, i = [], 0
+    for b in [1, 300, 2, 4096, 17, 1000]:
+        if i >= len(frags):
+            break
+        b = min(b, len(frags) - i)
+        bounds.append((i, b))
+        i += b
+    if i < len(frags):
+        bounds.append((i, len(frags) - i))
+    pend = 0
+    for lo, b in bounds:
+        while True:
+            r = lib.fd_ed25519_gpu_stage_submit(st, _vp(arena), len(arena), fr[lo:].ctypes.data, b,
+                                                res[lo:].ctypes.data, sig[lo:].ctypes.data)
+            if r != -104:       # FD_ED25519_GPU_ERR_BUSY: complete the oldest first
+                break
+            assert lib.fd_ed25519_gpu_stage_poll(st, 1) == 0
+        assert r == 0, r
+        assert lib.fd_ed25519_gpu_stage_pending(st) <= 2
+    while lib.fd_ed25519_gpu_stage_pending(st):
+        assert lib.fd_ed25519_gpu_stage_poll(st, 1) == 0
+    lib.fd_ed25519_gpu_stage_delete(st)
+    bad = np.nonzero((res != exp_res) | (sig != exp_tag))[0]
+    assert len(bad) == 0, [(int(j), int(res[j]), int(exp_res[j])) for j in bad[:10]]
+
+
+@pytest.mark.gpu
+def test_offload_link_served_on_gpu_vs_reference_tile(gpu, ref):
+    """The offload process's loop (fd_verify_offload_serve, here on a thread)
+    behind the shared-memory link: a client publishes 4000 frags one by one
+    (retrying on a full ring / frag area), reads the results by seq; they
+    equal the sequential reference tile's."""
+    rng = np.random.default_rng(78)
+    arena, frags = _random_frag_stream(rng, 1500, 4000)
+    exp_res, exp_tag = ref_seq(ref, arena, frags)
+    name = "/fdvo_gpu_%d" % os.getpid()
+    srv = fa.OffloadLink.create(name, depth=1024, dcache_sz=1 << 20)
+    cli = fa.OffloadLink.join(name)
+    th = fa.ServeThread(srv, gpu, fa.TCache(), max_batch=512, threads=2)
+    got_r = np.zeros(len(frags), np.int8)
+    got_s = np.zeros(len(frags), np.uint64)
+    nxt = 0
+    import time
+    t0 = time.time()
+    for i in range(len(frags)):
+        f = arena[int(frags["off"][i]):int(frags["off"][i]) + int(frags["sz"][i])].tobytes()
+        while True:
+            # a result slot is reused when seq + depth is published: read first
+            s = cli.publish(f) if i - nxt < 1024 else fa.offload.ERR_FULL
+            if s != fa.offload.ERR_FULL:
+                break
+            st_, r, g = cli.result(nxt)
+            if st_ == 1:
+                got_r[nxt], got_s[nxt] = r, g
+                nxt += 1
+            assert time.time() - t0 < 90, "offload server stalled"
+        assert s == i
+        while nxt <= i:              # drain whatever is ready
+            st_, r, g = cli.result(nxt)
+            if st_ != 1:
+                break
+            got_r[nxt], got_s[nxt] = r, g
+            nxt += 1
+    while nxt < len(frags):
+        st_, r, g = cli.result(nxt)
+        assert st_ in (0, 1)
+        if st_ == 1:
+            got_r[nxt], got_s[nxt] = r, g
+            nxt += 1
+        assert time.time() - t0 < 90, "offload server stalled"
+    cli.halt()
+    stats = th.join(30)
+    cli.close()
+    srv.close()
+    assert stats[1] == len(frags)
+    bad = np.nonzero((got_r != exp_res) | (got_s != exp_tag))[0]
+    assert len(bad) == 0, [(int(j), int(got_r[j]), int(exp_res[j])) for j in bad[:10]]
