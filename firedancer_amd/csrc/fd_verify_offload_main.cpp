@@ -42,6 +42,9 @@ int main( int argc, char ** argv ) {
   fd_ed25519_gpu_t * ctx = fd_ed25519_gpu_new( gpus, batch * 4u );   /* larger batches are chunked internally */
   fd_ed25519_gpu_tcache_t * tc = fd_ed25519_gpu_tcache_new( tdepth, tmap );
   if( !ctx || !tc ) { fprintf( stderr, "GPU context / tcache creation failed\n" ); fd_verify_offload_unlink( name ); return 1; }
+  uint8_t * dc = fd_verify_offload_dcache( off );
+  int pinned = !fd_ed25519_gpu_host_register( ctx, dc, fd_verify_offload_dcache_sz( off ) );
+  fprintf( stderr, "fd_verify_offload_server: frag area %s\n", pinned ? "page-locked" : "pageable (register failed)" );
   fprintf( stderr, "fd_verify_offload_server: serving %s (depth %lu, frag area %lu MB, batch %lu)\n",
            name, (unsigned long)depth, (unsigned long)dcache_mb, (unsigned long)batch );
   fflush( stderr );
@@ -51,6 +54,7 @@ int main( int argc, char ** argv ) {
   int err = fd_verify_offload_serve( off, ctx, tc, batch, threads, stats );
   printf( "{\"err\": %d, \"batches\": %lu, \"frags\": %lu, \"max_batch\": %lu, \"idle_polls\": %lu}\n", err,
           (unsigned long)stats[0], (unsigned long)stats[1], (unsigned long)stats[2], (unsigned long)stats[3] );
+  if( pinned ) fd_ed25519_gpu_host_unregister( ctx, dc );
   fd_ed25519_gpu_tcache_delete( tc );
   fd_ed25519_gpu_delete( ctx );
   fd_verify_offload_leave( off );

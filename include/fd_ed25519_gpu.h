@@ -90,6 +90,12 @@ int fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t *        ctx,
                                  uint64_t                  desc_cnt,
                                  int8_t *                  out_code );
 
+/* Page-lock a host region (e.g. a workspace / dcache the arenas live in) for
+   every device of ctx, so the per-batch copies to HBM are direct DMA
+   (hipHostRegister, portable).  Unregister before freeing the region. */
+int fd_ed25519_gpu_host_register  ( fd_ed25519_gpu_t * ctx, void * p, uint64_t sz );
+int fd_ed25519_gpu_host_unregister( fd_ed25519_gpu_t * ctx, void * p );
+
 /* Asynchronous pair (wiredancer-style push model, src/wiredancer/c/wd_f1.h:71-112):
    submit enqueues the copies + kernels and returns; poll returns
    FD_ED25519_GPU_PENDING until every device finished, then FD_ED25519_GPU_OK
