@@ -19,6 +19,11 @@ CODES_REF = 1
 # fd_sha512_gpu_msg_t (8 bytes)
 SHA_MSG_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4")])
 
+# fd_ed25519_gpu_precompile_t (16 bytes): data span + the txn's instruction spans [lo, lo+cnt)
+PRECOMPILE_DTYPE = np.dtype([("data_off", "<u4"), ("data_sz", "<u4"), ("txn_instr_lo", "<u4"),
+                             ("txn_instr_cnt", "<u4")])
+SPAN_DTYPE = np.dtype([("off", "<u4"), ("sz", "<u4")])
+
 # fd_ed25519_desc_t (16 bytes, include/fd_ed25519_gpu.h)
 DESC_DTYPE = np.dtype([("sig_off", "<u4"), ("pub_off", "<u4"), ("msg_off", "<u4"),
                        ("msg_sz", "<u2"), ("txn_idx", "<u2")])
@@ -83,6 +88,9 @@ def load_lib():
     lib.fd_ed25519_gpu_frags_to_descs.restype = ctypes.c_int64
     lib.fd_ed25519_gpu_frags_to_descs.argtypes = [vp, u64, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_verify_frags.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_precompile_verify.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp]
+    lib.fd_ed25519_gpu_host_register.argtypes = [vp, vp, u64]
+    lib.fd_ed25519_gpu_host_unregister.argtypes = [vp, vp]
     lib.fd_ed25519_gpu_strerror.restype = ctypes.c_char_p
     lib.fd_ed25519_gpu_strerror.argtypes = [i32]
     _LIB = lib
@@ -213,6 +221,20 @@ class Ed25519Gpu:
         if r:
             raise GpuError("fd_ed25519_gpu_test_lattice: %s (%d)" % (strerror(r), r))
         return out
+
+    def precompile_verify(self, arena, arena_sz, instrs, spans):
+        """Batched fd_ed25519_program_execute: instrs PRECOMPILE_DTYPE, spans
+        SPAN_DTYPE (the transactions' instruction data) -> int32 results
+        (0 / -100 / -101 / -102, FD_EXECUTOR_SIGN_ERR_*)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        instrs = np.ascontiguousarray(instrs, dtype=PRECOMPILE_DTYPE)
+        spans = np.ascontiguousarray(spans, dtype=SPAN_DTYPE)
+        out = np.zeros(max(len(instrs), 1), np.int32)
+        r = self.lib.fd_ed25519_gpu_precompile_verify(self.ctx, _ptr(arena), arena_sz, _ptr(instrs), len(instrs),
+                                                      _ptr(spans), len(spans), _ptr(out))
+        if r:
+            raise GpuError("fd_ed25519_gpu_precompile_verify: %s (%d)" % (strerror(r), r))
+        return out[:len(instrs)]
 
     def sha512_batch(self, msgs):
         """Batched SHA-512 of a list of byte strings (mirror of fd_sha512_batch_add per message)."""

@@ -245,6 +245,40 @@ int  fd_ed25519_gpu_stage_submit ( fd_ed25519_gpu_stage_t * st, uint8_t const * 
 int  fd_ed25519_gpu_stage_poll   ( fd_ed25519_gpu_stage_t * st, int block );
 int  fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st );
 
+/* ---- Ed25519 precompile instructions ----------
+
+   Batched form of fd_ed25519_program_execute
+   (src/flamenco/runtime/program/fd_ed25519_program.c:70-122): for each
+   precompile instruction, its data (sig count, 14-byte offsets records
+   {sig_offset, sig_instr_idx, pubkey_offset, pubkey_instr_idx, msg_offset,
+   msg_data_sz, msg_instr_idx}) is walked in order, each record's spans taken
+   from this instruction's data (index 0xFFFF) or from instruction `index` of
+   its transaction, and out[j] gets the reference's result for instruction j
+   (values of FD_EXECUTOR_SIGN_ERR_*, src/flamenco/runtime/fd_executor.h:77-79):
+   the first failure in record order decides. */
+#define FD_ED25519_GPU_PRECOMPILE_OK                          (   0)
+#define FD_ED25519_GPU_PRECOMPILE_ERR_DATA_OFFSETS            (-100)
+#define FD_ED25519_GPU_PRECOMPILE_ERR_INSTRUCTION_DATA_SIZE   (-101)
+#define FD_ED25519_GPU_PRECOMPILE_ERR_SIGNATURE               (-102)
+
+typedef struct {
+  uint32_t off;        /* bytes from the arena base */
+  uint32_t sz;
+} fd_ed25519_gpu_span_t;
+
+typedef struct {
+  fd_ed25519_gpu_span_t data;            /* this precompile instruction's data */
+  uint32_t              txn_instr_lo;    /* its transaction's instructions' data: */
+  uint32_t              txn_instr_cnt;   /*   txn_instr[lo, lo + cnt), index order */
+} fd_ed25519_gpu_precompile_t;
+
+/* Host memory, synchronous; every span must lie in arena[0, arena_sz) (else
+   FD_ED25519_GPU_ERR_ARG, nothing launched). */
+int fd_ed25519_gpu_precompile_verify( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                                      fd_ed25519_gpu_precompile_t const * instr, uint64_t n,
+                                      fd_ed25519_gpu_span_t const * txn_instr, uint64_t txn_instr_cnt,
+                                      int * out );
+
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
    u32 words each, k < l) on the context's first device.  out: n records of

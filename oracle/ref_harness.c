@@ -261,3 +261,55 @@ fdref_tcache_seq( ulong depth, ulong map_cnt, ulong const * ops, ulong n, int * 
   free( fd_tcache_delete( fd_tcache_leave( tcache ) ) );
   return (int)tmap_cnt;
 }
+
+/* ---- ed25519 precompile --------------------------
+
+   fdref_ed25519_program: fd_ed25519_program_execute
+   (src/flamenco/runtime/program/fd_ed25519_program.c:70-122) and
+   _get_instr_data (:32-68) restated line for line (the originals take an
+   fd_exec_instr_ctx_t, which drags in the whole runtime), over the
+   REFERENCE fd_ed25519_verify.  data/data_sz: the precompile instruction's
+   data; txn_instr: (pointer, size) of the transaction's instructions' data
+   for index != 0xFFFF.  Returns 0 / -100 / -101 / -102
+   (FD_EXECUTOR_SIGN_ERR_*, src/flamenco/runtime/fd_executor.h:77-79). */
+
+static int
+fdref_get_instr_data( uchar const * data, ulong data_sz, uchar const * const * txn_instr, ulong const * txn_instr_sz,
+                      ulong txn_instr_cnt, ulong index, ulong offset, ulong sz, uchar const ** res ) {
+  uchar const * d; ulong dsz;
+  if( index==0xFFFFUL ) { d = data; dsz = data_sz; }                              /* :44-49 */
+  else {
+    if( index>=txn_instr_cnt ) return -100;                                      /* :56-57 */
+    d = txn_instr[ index ]; dsz = txn_instr_sz[ index ];                         /* :59-61 */
+  }
+  if( offset+sz>dsz ) return -100;                                               /* :65-66 */
+  *res = d + offset;
+  return 0;
+}
+
+int
+fdref_ed25519_program( uchar const * data, ulong data_sz, uchar const * const * txn_instr,
+                       ulong const * txn_instr_sz, ulong txn_instr_cnt ) {
+  if( data_sz<2UL ) return -101;                                                 /* :76-77 */
+  ulong sig_cnt = data[0];
+  ulong off     = 2UL;
+  for( ulong i=0UL; i<sig_cnt; i++ ) {
+    if( off+14UL>data_sz ) return -101;                                          /* :83-84 */
+    uchar const * so = data + off;
+    off += 14UL;
+    ushort sig_offset, sig_idx, pub_offset, pub_idx, msg_offset, msg_sz, msg_idx;
+    memcpy( &sig_offset, so+ 0, 2 ); memcpy( &sig_idx, so+ 2, 2 );
+    memcpy( &pub_offset, so+ 4, 2 ); memcpy( &pub_idx, so+ 6, 2 );
+    memcpy( &msg_offset, so+ 8, 2 ); memcpy( &msg_sz,  so+10, 2 ); memcpy( &msg_idx, so+12, 2 );
+    uchar const * sig = NULL, * pub = NULL, * msg = NULL;
+    int err = fdref_get_instr_data( data, data_sz, txn_instr, txn_instr_sz, txn_instr_cnt, sig_idx, sig_offset, 64UL, &sig );
+    if( err ) return err;
+    err = fdref_get_instr_data( data, data_sz, txn_instr, txn_instr_sz, txn_instr_cnt, pub_idx, pub_offset, 32UL, &pub );
+    if( err ) return err;
+    err = fdref_get_instr_data( data, data_sz, txn_instr, txn_instr_sz, txn_instr_cnt, msg_idx, msg_offset, msg_sz, &msg );
+    if( err ) return err;
+    fd_sha512_t sha[1];
+    if( fd_ed25519_verify( msg, msg_sz, sig, pub, sha )!=FD_ED25519_SUCCESS ) return -102;   /* :115-117 */
+  }
+  return 0;
+}
