@@ -171,6 +171,10 @@ __device__ __forceinline__ void vtab_ptrs( uint32_t const * vtab, uint64_t cap, 
   uint64_t idx = (uint64_t)e * cap + t;
   *m  = (uint4 const *)(vtab + idx * 32u);
   *tl = (uint4 const *)(vtab + (uint64_t)FD_VTAB_N * cap * 32u + idx * 8u);
+  if( !e ) {   /* the identity: one shared record after both regions (written by the host) */
+    uint32_t const * id = vtab + (uint64_t)FD_VTAB_N * cap * 40u;
+    *m = (uint4 const *)id; *tl = (uint4 const *)(id + 32);
+  }
 }
 
 __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint64_t t, int e, ge_cached const & c ) {
@@ -193,9 +197,7 @@ __device__ __forceinline__ void vtab_build( uint32_t * vtab, uint64_t cap, uint6
   ge_p3 nQ = Q;
   { fe x; fe_neg( x, Q.X ); fe_carry( nQ.X, x ); fe_neg( x, Q.T ); fe_carry( nQ.T, x ); }
   ge_cached c;
-  ge_p3 id; ge_identity( id );
-  ge_to_cached( c, id );  vtab_store( vtab, cap, t, 0, c );
-  ge_to_cached( c, nQ );  vtab_store( vtab, cap, t, 1, c );
+  ge_to_cached( c, nQ );  vtab_store( vtab, cap, t, 1, c );   /* entry 0 = the shared identity record */
   ge_precomp nQp;
   { fe d2; fe_const_d2( d2 ); fe_add_r( nQp.YpX, nQ.Y, nQ.X ); fe_sub_r( nQp.YmX, nQ.Y, nQ.X ); fe_mul( nQp.T2d, nQ.T, d2 ); }
   FE_FENCE();
