@@ -233,10 +233,17 @@ def main():
                        "msg_sz": args.msg_sz if args.config == 2 else None, "parallelism": "shard-per-gpu x%d" % world},
             "roofline": {"bound": "valu-int32", "achieved": achieved / 1e12, "peak": peak / 1e12,
                          "unit": "T MAC/s (32x32->64 multiply-adds, W=%.4g per verify)" % W_MAC,
-                         "frac": achieved / peak, "traffic": pmc_traffic(n),
+                         "frac": achieved / peak, "traffic": pmc_traffic(n) if args.config == 2 else None,
                          "kernel_ms": launch_ms},
             "cpu_baseline": None,
         }
+        # The same launch against the HBM roofline (not the bound: ~1/6 of the ~8 TB/s peak),
+        # from the PMC-measured bytes per launch of profiles/r01/pmc_traffic.json.
+        t = pmc_traffic(n) if args.config == 2 else None
+        if t:
+            gbs = t / (launch_ms * 1e-3) / 1e9
+            line["roofline_hbm"] = {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
+                                    "frac": gbs / 8000.0, "traffic": t}
         if args.config != 2:   # the roofline numerator W is defined for valid 200-B verifies only
             line["roofline"]["frac_note"] = "W-based numerator is for valid 200-B verifies (config 2)"
         if world == 1 and not args.no_cpu:
