@@ -69,6 +69,10 @@ def build_workload(n, msg_sz, seed, n_keys=None):
         "(seed %d), RFC 8032-signed by tools/synth.py, all valid" % (n, n_keys, what, 1234 + seed)
 
 
+def desc_pub(arena, desc):
+    return [arena[int(o):int(o) + 32].tobytes() for o in desc["pub_off"]]
+
+
 def build_adversarial(n):
     """Config 4: every committed golden record (the reference's Wycheproof,
     CCTV and malleability vectors plus the generated adversarial classes,
@@ -146,6 +150,9 @@ def main():
                          "Uniform{0..1232}-B messages, split over the GPUs (strong scaling); "
                          "4: the adversarial golden mix tiled to --batch per GPU")
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--hot-keys", type=int, default=0,
+                    help="config 2 with this many distinct signers, all in the hot-key cache "
+                         "(vote-like traffic; fd_ed25519_gpu_keycache_*)")
     ap.add_argument("--msg-sz", type=int, default=200)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -172,8 +179,14 @@ def main():
         arena, desc, sz, expect, data_desc = build_adversarial(n)
     else:
         n = args.batch or 65536
-        arena, desc, sz, expect, data_desc = build_workload(n, args.msg_sz, seed=rank)
+        arena, desc, sz, expect, data_desc = build_workload(n, args.msg_sz, seed=rank,
+                                                            n_keys=args.hot_keys or None)
     g = fa.Ed25519Gpu(device_mask=1 << local, max_batch=n)
+    if args.hot_keys:
+        keys = sorted(set(desc_pub(arena, desc)))
+        g.keycache_reserve(len(keys))
+        g.keycache_add(keys)
+        data_desc += "; all %d signers in the hot-key cache" % len(keys)
     d_arena = torch.from_numpy(arena).to(dev)
     d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
     d_out = torch.zeros(n, dtype=torch.int8, device=dev)
@@ -233,13 +246,13 @@ def main():
                        "msg_sz": args.msg_sz if args.config == 2 else None, "parallelism": "shard-per-gpu x%d" % world},
             "roofline": {"bound": "valu-int32", "achieved": achieved / 1e12, "peak": peak / 1e12,
                          "unit": "T MAC/s (32x32->64 multiply-adds, W=%.4g per verify)" % W_MAC,
-                         "frac": achieved / peak, "traffic": pmc_traffic(n) if args.config == 2 else None,
+                         "frac": achieved / peak, "traffic": pmc_traffic(n) if args.config == 2 and not args.hot_keys else None,
                          "kernel_ms": launch_ms},
             "cpu_baseline": None,
         }
         # The same launch against the HBM roofline (not the bound: ~1/6 of the ~8 TB/s peak),
         # from the PMC-measured bytes per launch of profiles/r01/pmc_traffic.json.
-        t = pmc_traffic(n) if args.config == 2 else None
+        t = pmc_traffic(n) if args.config == 2 and not args.hot_keys else None
         if t:
             gbs = t / (launch_ms * 1e-3) / 1e9
             line["roofline_hbm"] = {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",

@@ -21,6 +21,19 @@
 #define FD_VTAB_WORDS     40           /* u32 per entry (4 fe)                        */
 #define FD_NDIG_MAX       64           /* 4-bit windows of a <= 256-bit scalar        */
 
+/* Hot-key cache (per device): for each cached public key A, the comb table
+   [j](16^p (-A)), p < 64, j in [1, 8], affine precomputed form (Y+X, Y-X,
+   2dXY) in 128-B records (64 KB per key), plus a 16-word meta record
+   (the key's 8 words, decode / small-order status).  Lookup: open
+   addressing on a seeded hash of the key's first 8 bytes. */
+#define FD_KTAB_POS       64
+#define FD_KTAB_ENT       8
+#define FD_KTAB_WORDS     (FD_KTAB_POS * FD_KTAB_ENT * 32)   /* u32 per key */
+#define FD_KMETA_WORDS    16
+#define FD_KST_OK_REF     1u           /* decodes under the portable build's rule   */
+#define FD_KST_OK_AVX     2u           /* decodes under the AVX-512 build's rule     */
+#define FD_KST_SMALL      4u           /* small order                                */
+
 /* LDS digit rows ([row][slot] bytes) */
 #define FD_ROW_U          0            /* signed 4-bit digits of u (sign folded in)   */
 #define FD_ROW_V          64           /* signed 4-bit digits of v                    */
@@ -40,6 +53,29 @@ struct verify_args {
   uint64_t                  vtab_cap;  /* tables                                   */
   int                       ref_codes;
   unsigned long long *      stamps;    /* FD_PHASE_STAMPS builds only: per-phase cycle sums */
+  /* descriptor lists (hot-key cache split): lane i handles desc[idx[i]] for
+     i < *cnt; idx == NULL: lane i handles desc[i] for i < n */
+  uint32_t const *          idx;
+  uint32_t const *          cnt;
+  uint32_t const *          slot;      /* cached kernel: key slot of list entry i */
+  uint32_t const *          ktab;      /* cached kernel: FD_KTAB_WORDS per slot (+ identity record) */
+  uint32_t const *          kmeta;     /* cached kernel: FD_KMETA_WORDS per slot */
+  uint64_t                  kcap;      /* slots */
+};
+
+struct kpart_args {
+  uint8_t const *           arena;
+  uint64_t                  arena_sz;
+  fd_ed25519_desc_t const * desc;
+  uint64_t                  n;
+  uint32_t const *          khash;     /* hsize entries: slot + 1, 0 = empty */
+  uint64_t                  hmask;
+  uint64_t                  seed;
+  uint32_t const *          kmeta;
+  uint32_t *                hit_idx;   /* out: desc indices whose key is cached */
+  uint32_t *                hit_slot;
+  uint32_t *                miss_idx;
+  uint32_t *                counts;    /* [0] hits, [1] misses (zeroed before launch) */
 };
 
 /* Kernel symbols in the code object (extern "C"). */
@@ -47,5 +83,22 @@ struct verify_args {
 #define FD_KERN_CTAB     "fd_ed25519_ctab_init"
 #define FD_KERN_LATTEST  "fd_ed25519_lattice_test_kernel"
 #define FD_KERN_SHA512   "fd_sha512_batch_kernel"
+#define FD_KERN_KBUILD   "fd_ed25519_ktab_build_kernel"
+#define FD_KERN_KPART    "fd_ed25519_kcache_part_kernel"
+#define FD_KERN_CACHED   "fd_ed25519_verify_cached_kernel"
+
+/* Seeded key hash shared by the host (slot assignment) and the device
+   (lookup): splitmix64 of the key's first 8 bytes xor seed. */
+static inline
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+uint64_t fd_kcache_hash( uint32_t w0, uint32_t w1, uint64_t seed ) {
+  uint64_t z = ((uint64_t)w1 << 32 | w0) ^ seed;
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
 
 #endif /* FD_ED25519_GPU_ABI_H */

@@ -351,12 +351,17 @@ fd_ed25519_verify_kernel( verify_args args ) {
   STAMP( 0 );
   uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)tid;
   uint64_t cap = args.vtab_cap;
+  /* List form (hot-key cache split): the count is known on the device only;
+     whole waves past it leave at once (wave-uniform). */
+  uint64_t nn = args.cnt ? (uint64_t)*args.cnt : args.n;
+  if( (gid & ~(uint64_t)63) >= nn ) return;
   /* Every lane stays to the wave-wide window count below (no early exit):
      lanes past n or with a bad descriptor take the no-work path.  The
      descriptor / signature / key loads are issued first. */
-  bool valid = gid < args.n;
+  bool valid = gid < nn;
+  uint64_t di = valid ? (args.idx ? (uint64_t)args.idx[ gid ] : gid) : 0u;
   fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
-  if( valid ) d = args.desc[ gid ];
+  if( valid ) d = args.desc[ di ];
   uint64_t asz = args.arena_sz;
   bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
                  (uint64_t)d.msg_off + d.msg_sz <= asz;
@@ -469,7 +474,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
     int ey = fe_is_zero( dl );
     code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
   }
-  args.out[ gid ] = (int8_t)code;
+  args.out[ di ] = (int8_t)code;
 #ifdef FD_PHASE_STAMPS
   STAMP( 6 );
   if( args.stamps && (tid & 63) == 0 ) {
@@ -538,6 +543,211 @@ fd_sha512_batch_kernel( uint8_t const * arena, uint64_t arena_sz, fd_sha512_gpu_
   for( int q=0; q<4; q++ )
     o[q] = make_uint4( sha_bswap32( (uint32_t)(h[2*q]   >> 32) ), sha_bswap32( (uint32_t)h[2*q]   ),
                        sha_bswap32( (uint32_t)(h[2*q+1] >> 32) ), sha_bswap32( (uint32_t)h[2*q+1] ) );
+}
+
+/* ------------------------------------------------------------------ hot-key cache */
+
+/* Build the comb tables of newly cached keys, one key per lane: decode A
+   under both builds' rules, small-order status, then [j](16^p (-A)) for
+   p < 64, j in [1, 8] as affine precomputed records (one inversion each:
+   this runs once per key, at fd_ed25519_gpu_keycache_add). */
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_ed25519_ktab_build_kernel( uint32_t * ktab, uint32_t * kmeta, uint32_t const * pubs, uint32_t const * slots,
+                              uint64_t n ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  uint32_t pub[ 8 ];
+#pragma unroll
+  for( int j=0; j<8; j++ ) pub[j] = pubs[ i*8u + (uint64_t)j ];
+  uint64_t slot = slots[ i ];
+  ge_p3 A, A2;
+  int ok_ref = ge_decode( A, pub, false );
+  int ok_avx = ge_decode( A2, pub, true );
+  int sm = ge_affine_small_order( A );
+  uint32_t * m = kmeta + slot * FD_KMETA_WORDS;
+#pragma unroll
+  for( int j=0; j<8; j++ ) m[j] = pub[j];
+  m[8] = (ok_ref ? FD_KST_OK_REF : 0u) | (ok_avx ? FD_KST_OK_AVX : 0u) | (sm ? FD_KST_SMALL : 0u);
+  if( !ok_ref || sm ) return;                       /* such a key never reaches the equation */
+  ge_p3 base = A;
+  { fe x; fe_neg( x, A.X ); fe_carry( base.X, x ); fe_neg( x, A.T ); fe_carry( base.T, x ); }
+  uint32_t * kt = ktab + slot * (uint64_t)FD_KTAB_WORDS;
+#pragma unroll 1
+  for( int p=0; p<FD_KTAB_POS; p++ ) {
+    ge_precomp bp; ge_affine_precomp( bp, base );   /* base := affine */
+    ge_p3 P = base;
+#pragma unroll 1
+    for( int j=1; j<=FD_KTAB_ENT; j++ ) {
+      if( j == 2 ) ge_dbl( P, base, true );
+      else if( j > 2 ) ge_madd( P, P, bp, true );
+      ge_precomp e;
+      if( j == 1 ) e = bp;
+      else ge_affine_precomp( e, P );
+      uint32_t * r = kt + (uint64_t)(p*FD_KTAB_ENT + (j-1)) * 32u;
+#pragma unroll
+      for( int w=0; w<10; w++ ) { r[w] = e.YpX.v[w]; r[10+w] = e.YmX.v[w]; r[20+w] = e.T2d.v[w]; }
+      r[30] = 0u; r[31] = 0u;
+    }
+    ge_dbl( P, P, true );                           /* [16] base: the next position's base */
+    base = P;
+  }
+}
+
+/* Split a batch by key: descriptors whose public key is cached go to the
+   hit list (with its slot), the rest (and out-of-arena descriptors) to the
+   miss list.  One lane per descriptor; list appends are wave-aggregated. */
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_ed25519_kcache_part_kernel( kpart_args a ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool valid = i < a.n;
+  int64_t slot = -1;
+  if( valid ) {
+    fd_ed25519_desc_t d = a.desc[ i ];
+    if( (uint64_t)d.pub_off + 32u <= a.arena_sz ) {
+      uint32_t lim_dw = (uint32_t)((a.arena_sz + 3u) >> 2) + 1u;
+      uint32_t pub[ 8 ];
+      load_words<8>( pub, a.arena, d.pub_off, lim_dw );
+      uint64_t h = fd_kcache_hash( pub[0], pub[1], a.seed ) & a.hmask;
+      for( uint64_t probe=0; probe<=a.hmask; probe++ ) {
+        uint32_t e = a.khash[ h ];
+        if( !e ) break;
+        uint32_t const * m = a.kmeta + (uint64_t)(e - 1u) * FD_KMETA_WORDS;
+        uint32_t diff = 0u;
+#pragma unroll
+        for( int j=0; j<8; j++ ) diff |= m[j] ^ pub[j];
+        if( !diff ) { slot = (int64_t)(e - 1u); break; }
+        h = (h + 1u) & a.hmask;
+      }
+    }
+  }
+  bool hit = valid && slot >= 0, miss = valid && slot < 0;
+  uint64_t bh = __ballot( hit ), bm = __ballot( miss );
+  uint32_t lane = threadIdx.x & 63u;
+  uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+  uint32_t base_h = 0u, base_m = 0u;
+  if( lane == 0u ) {
+    if( bh ) base_h = atomicAdd( &a.counts[0], (uint32_t)__popcll( bh ) );
+    if( bm ) base_m = atomicAdd( &a.counts[1], (uint32_t)__popcll( bm ) );
+  }
+  base_h = __shfl( base_h, 0 ); base_m = __shfl( base_m, 0 );
+  if( hit )  { uint32_t o = base_h + (uint32_t)__popcll( bh & below ); a.hit_idx[ o ] = (uint32_t)i; a.hit_slot[ o ] = (uint32_t)slot; }
+  if( miss ) { uint32_t o = base_m + (uint32_t)__popcll( bm & below ); a.miss_idx[ o ] = (uint32_t)i; }
+}
+
+/* Key-table entry j (digit d != 0: entry |d|; d == 0: the identity record
+   after the slots) of position p. */
+__device__ __forceinline__ void ktab_fetch( uint32_t w[ 32 ], uint32_t const * ktab, uint64_t kcap, uint64_t slot,
+                                            int p, int d ) {
+  uint32_t e = (uint32_t)(d < 0 ? -d : d);
+  uint32_t const * r = e ? ktab + slot * (uint64_t)FD_KTAB_WORDS + (uint64_t)(p*FD_KTAB_ENT + (int)e - 1) * 32u
+                         : ktab + kcap * (uint64_t)FD_KTAB_WORDS;
+  uint4 const * q = (uint4 const *)r;
+#pragma unroll
+  for( int j=0; j<8; j++ ) { uint4 v = q[j]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
+}
+
+/* Signed 4-bit digit p of a 256-bit scalar, carry threaded by the caller
+   (digits in [-8, 7], the top one keeps its carry). */
+__device__ __forceinline__ int nib_digit( uint32_t const x[ 8 ], int p, int * c ) {
+  int d = (int)((x[p>>3] >> (4*(p&7))) & 15u) + *c;
+  *c = d >= 8 && p < FD_KTAB_POS-1;
+  return d - (*c << 4);
+}
+
+/* Verify with a cached key: the reference equation itself,
+   [S]B + [k](-A) == R (fd_ed25519_user.c:208-228), as 64 mixed additions
+   from the key's comb table plus 16 from the fixed-base comb table -- no
+   doublings, no lattice, no decode of A, no per-signature tables -- then
+   the projective compare against the decoded R.  Codes follow the same
+   check order as the main kernel (the key's decode / small-order status
+   comes from the cache). */
+extern "C" __global__ void __launch_bounds__( FD_VERIFY_BLOCK, FD_VERIFY_WAVES_PER_EU )
+fd_ed25519_verify_cached_kernel( verify_args args ) {
+  uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)threadIdx.x;
+  uint64_t nn = (uint64_t)*args.cnt;
+  if( (gid & ~(uint64_t)63) >= nn ) return;
+  bool valid = gid < nn;
+  uint64_t di = valid ? (uint64_t)args.idx[ gid ] : 0u;
+  uint64_t slot = valid ? (uint64_t)args.slot[ gid ] : 0u;
+  fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
+  if( valid ) d = args.desc[ di ];
+  uint64_t asz = args.arena_sz;
+  bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
+                 (uint64_t)d.msg_off + d.msg_sz <= asz;
+  uint32_t lim_dw = (uint32_t)((asz + 3u) >> 2) + 1u;
+  uint32_t sig[ 16 ], pub[ 8 ];
+#pragma unroll
+  for( int j=0; j<16; j++ ) sig[j] = 0u;
+#pragma unroll
+  for( int j=0; j<8; j++ ) pub[j] = 0u;
+  if( desc_ok ) {
+    load_words<16>( sig, args.arena, d.sig_off, lim_dw );
+    load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
+  }
+  uint32_t st = valid ? args.kmeta[ slot * FD_KMETA_WORDS + 8u ] : 0u;
+  bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                           /* :157-159 */
+  bool live  = desc_ok && !bad_s;
+  uint32_t k[ 8 ];
+#pragma unroll
+  for( int j=0; j<8; j++ ) k[j] = 0u;
+  if( live ) hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );   /* :203-206 */
+  FE_FENCE();
+  ge_p3 R;
+  int okR = ge_decode( R, sig, !args.ref_codes );                        /* :162 (R after A) */
+  int smR = ge_affine_small_order( R );
+  bool okA = (st & (args.ref_codes ? FD_KST_OK_REF : FD_KST_OK_AVX)) != 0u;
+  int code;
+  if     ( !desc_ok            ) code = FD_ED25519_GPU_CODE_BAD_DESC;
+  else if( bad_s               ) code = FD_ED25519_ERR_SIG;
+  else if( !okA                ) code = args.ref_codes ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;   /* :190-192 */
+  else if( !okR                ) code = FD_ED25519_ERR_SIG;
+  else if( st & FD_KST_SMALL   ) code = FD_ED25519_ERR_PUBKEY;                                        /* :193-195 */
+  else if( smR                 ) code = FD_ED25519_ERR_SIG;                                           /* :196-198 */
+  else                           code = 0;
+  bool run = code == 0;
+  if( __any( run ) ) {
+    /* lanes not running the equation use slot 0 / digit 0 (valid memory) */
+    uint64_t sl = run ? slot : 0u;
+    uint32_t kk[ 8 ], ss[ 8 ];
+#pragma unroll
+    for( int j=0; j<8; j++ ) { kk[j] = run ? k[j] : 0u; ss[j] = run ? sig[8+j] : 0u; }
+    ge_p3 acc; ge_identity( acc );
+    uint32_t raw[ 32 ];
+    int ck = 0;
+    int dk = nib_digit( kk, 0, &ck );
+    ktab_fetch( raw, args.ktab, args.kcap, sl, 0, dk );
+#pragma unroll 1
+    for( int p=0; p<FD_KTAB_POS; p++ ) {
+      ge_precomp e;
+      ctab_finish( e, raw, dk );
+      if( p + 1 < FD_KTAB_POS ) { dk = nib_digit( kk, p + 1, &ck ); ktab_fetch( raw, args.ktab, args.kcap, sl, p + 1, dk ); }
+      FE_FENCE();
+      ge_madd( acc, acc, e, true );
+      FE_FENCE();
+    }
+    /* + [S]B from the fixed-base comb table (signed 16-bit windows of S) */
+    int cs = 0, ds;
+    {
+      int dd = (int)(ss[0] & 0xffffu); cs = dd >= 32768; ds = dd - (cs << 16);
+    }
+    ctab_fetch( raw, args.ctab, 0, ds );
+#pragma unroll 1
+    for( int q=0; q<FD_CTAB_POS; q++ ) {
+      ge_precomp e;
+      ctab_finish( e, raw, ds );
+      if( q + 1 < FD_CTAB_POS ) {
+        int dd = (int)((ss[(q+1)>>1] >> (16*((q+1)&1))) & 0xffffu) + cs;
+        cs = dd >= 32768 && q + 1 < FD_CTAB_POS-1;
+        ds = dd - (cs << 16);
+        ctab_fetch( raw, args.ctab, q + 1, ds );
+      }
+      FE_FENCE();
+      ge_madd( acc, acc, e, q + 1 < FD_CTAB_POS );
+      FE_FENCE();
+    }
+    if( run ) code = ge_eq_z1( acc, R ) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;   /* :225-228 */
+  }
+  if( valid ) args.out[ di ] = (int8_t)code;
 }
 
 /* Self-test kernel (tests only, fd_ed25519_gpu_test_lattice): the device

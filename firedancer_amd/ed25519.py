@@ -91,6 +91,12 @@ def load_lib():
     lib.fd_ed25519_gpu_precompile_verify.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp]
     lib.fd_ed25519_gpu_host_register.argtypes = [vp, vp, u64]
     lib.fd_ed25519_gpu_host_unregister.argtypes = [vp, vp]
+    lib.fd_ed25519_gpu_keycache_reserve.argtypes = [vp, u64]
+    lib.fd_ed25519_gpu_keycache_add.restype = ctypes.c_int64
+    lib.fd_ed25519_gpu_keycache_add.argtypes = [vp, ctypes.c_char_p, u64]
+    lib.fd_ed25519_gpu_keycache_cnt.restype = u64
+    lib.fd_ed25519_gpu_keycache_cnt.argtypes = [vp]
+    lib.fd_ed25519_gpu_keycache_clear.argtypes = [vp]
     lib.fd_ed25519_gpu_strerror.restype = ctypes.c_char_p
     lib.fd_ed25519_gpu_strerror.argtypes = [i32]
     _LIB = lib
@@ -221,6 +227,28 @@ class Ed25519Gpu:
         if r:
             raise GpuError("fd_ed25519_gpu_test_lattice: %s (%d)" % (strerror(r), r))
         return out
+
+    def keycache_reserve(self, capacity):
+        """Size the hot-key cache (64 KB of HBM per key per device); clears it."""
+        r = self.lib.fd_ed25519_gpu_keycache_reserve(self.ctx, capacity)
+        if r:
+            raise GpuError("fd_ed25519_gpu_keycache_reserve: %s (%d)" % (strerror(r), r))
+
+    def keycache_add(self, pubkeys):
+        """Cache public keys (iterable of 32-byte strings) -> number newly added."""
+        blob = b"".join(bytes(k) for k in pubkeys)
+        r = self.lib.fd_ed25519_gpu_keycache_add(self.ctx, blob, len(blob) // 32)
+        if r < 0:
+            raise GpuError("fd_ed25519_gpu_keycache_add: %s (%d)" % (strerror(r), r))
+        return int(r)
+
+    def keycache_cnt(self):
+        return int(self.lib.fd_ed25519_gpu_keycache_cnt(self.ctx))
+
+    def keycache_clear(self):
+        r = self.lib.fd_ed25519_gpu_keycache_clear(self.ctx)
+        if r:
+            raise GpuError("fd_ed25519_gpu_keycache_clear: %s (%d)" % (strerror(r), r))
 
     def precompile_verify(self, arena, arena_sz, instrs, spans):
         """Batched fd_ed25519_program_execute: instrs PRECOMPILE_DTYPE, spans

@@ -96,6 +96,21 @@ int fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t *        ctx,
 int fd_ed25519_gpu_host_register  ( fd_ed25519_gpu_t * ctx, void * p, uint64_t sz );
 int fd_ed25519_gpu_host_unregister( fd_ed25519_gpu_t * ctx, void * p );
 
+/* Hot-key cache.  Solana traffic is dominated by a few thousand repeat
+   signers (validators' vote authorities), so the context can keep, per
+   cached public key A, a comb table of [j](16^p (-A)) (64 KB of HBM per
+   key, built once).  A signature whose key is cached is verified as the
+   reference's own equation [S]B + [k](-A) == R with 80 table additions and
+   no doublings; the batch is split by key on the device, codes are
+   unchanged (bit-exact either way).  reserve sizes the cache (per device:
+   capacity x 64 KB + lists for max_batch signatures; clears it); add
+   inserts keys (32 B each; already-cached keys are skipped; stops when
+   full) and returns how many were added. */
+int      fd_ed25519_gpu_keycache_reserve( fd_ed25519_gpu_t * ctx, uint64_t capacity );
+int64_t  fd_ed25519_gpu_keycache_add    ( fd_ed25519_gpu_t * ctx, uint8_t const * pubkeys, uint64_t n );
+uint64_t fd_ed25519_gpu_keycache_cnt    ( fd_ed25519_gpu_t const * ctx );
+int      fd_ed25519_gpu_keycache_clear  ( fd_ed25519_gpu_t * ctx );
+
 /* Asynchronous pair (wiredancer-style push model, src/wiredancer/c/wd_f1.h:71-112):
    submit enqueues the copies + kernels and returns; poll returns
    FD_ED25519_GPU_PENDING until every device finished, then FD_ED25519_GPU_OK
