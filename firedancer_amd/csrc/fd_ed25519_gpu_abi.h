@@ -22,12 +22,14 @@
 #define FD_NDIG_MAX       64           /* 4-bit windows of a <= 256-bit scalar        */
 
 /* Hot-key cache (per device): for each cached public key A, the comb table
-   [j](16^p (-A)), p < 64, j in [1, 8], affine precomputed form (Y+X, Y-X,
-   2dXY) in 128-B records (64 KB per key), plus a 16-word meta record
-   (the key's 8 words, decode / small-order status).  Lookup: open
-   addressing on a seeded hash of the key's first 8 bytes. */
-#define FD_KTAB_POS       64
-#define FD_KTAB_ENT       8
+   [j](2^(FD_KTAB_WBITS p) (-A)), p < FD_KTAB_POS, j in [1, FD_KTAB_ENT],
+   affine precomputed form (Y+X, Y-X, 2dXY) in 128-B records (512 KB per key
+   with 8-bit windows), plus a 16-word meta record (the key's 8 words,
+   decode / small-order status).  Lookup: open addressing on a seeded hash
+   of the key's first 8 bytes. */
+#define FD_KTAB_WBITS     8
+#define FD_KTAB_POS       (256 / FD_KTAB_WBITS)               /* signed windows of k < 2^253 */
+#define FD_KTAB_ENT       (1 << (FD_KTAB_WBITS - 1))          /* |digit| in [1, 2^(w-1)]     */
 #define FD_KTAB_WORDS     (FD_KTAB_POS * FD_KTAB_ENT * 32)   /* u32 per key */
 #define FD_KMETA_WORDS    16
 #define FD_KST_OK_REF     1u           /* decodes under the portable build's rule   */

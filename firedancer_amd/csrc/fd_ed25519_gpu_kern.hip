@@ -548,9 +548,9 @@ fd_sha512_batch_kernel( uint8_t const * arena, uint64_t arena_sz, fd_sha512_gpu_
 /* ------------------------------------------------------------------ hot-key cache */
 
 /* Build the comb tables of newly cached keys, one key per lane: decode A
-   under both builds' rules, small-order status, then [j](16^p (-A)) for
-   p < 64, j in [1, 8] as affine precomputed records (one inversion each:
-   this runs once per key, at fd_ed25519_gpu_keycache_add). */
+   under both builds' rules, small-order status, then [j](2^(w p) (-A)) for
+   p < FD_KTAB_POS, j in [1, FD_KTAB_ENT] as affine precomputed records (one
+   inversion each: this runs once per key, at fd_ed25519_gpu_keycache_add). */
 extern "C" __global__ void __launch_bounds__( 256 )
 fd_ed25519_ktab_build_kernel( uint32_t * ktab, uint32_t * kmeta, uint32_t const * pubs, uint32_t const * slots,
                               uint64_t n ) {
@@ -588,7 +588,7 @@ fd_ed25519_ktab_build_kernel( uint32_t * ktab, uint32_t * kmeta, uint32_t const 
       for( int w=0; w<10; w++ ) { r[w] = e.YpX.v[w]; r[10+w] = e.YmX.v[w]; r[20+w] = e.T2d.v[w]; }
       r[30] = 0u; r[31] = 0u;
     }
-    ge_dbl( P, P, true );                           /* [16] base: the next position's base */
+    ge_dbl( P, P, true );                           /* [2^w] base: the next position's base */
     base = P;
   }
 }
@@ -646,16 +646,18 @@ __device__ __forceinline__ void ktab_fetch( uint32_t w[ 32 ], uint32_t const * k
   for( int j=0; j<8; j++ ) { uint4 v = q[j]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
 }
 
-/* Signed 4-bit digit p of a 256-bit scalar, carry threaded by the caller
-   (digits in [-8, 7], the top one keeps its carry). */
+/* Signed w-bit digit p of a 256-bit scalar (w = FD_KTAB_WBITS divides 32),
+   carry threaded by the caller (digits in [-2^(w-1), 2^(w-1)), the top one
+   keeps its carry). */
 __device__ __forceinline__ int nib_digit( uint32_t const x[ 8 ], int p, int * c ) {
-  int d = (int)((x[p>>3] >> (4*(p&7))) & 15u) + *c;
-  *c = d >= 8 && p < FD_KTAB_POS-1;
-  return d - (*c << 4);
+  int const w = FD_KTAB_WBITS, per = 32 / FD_KTAB_WBITS;
+  int d = (int)((x[p/per] >> (w*(p%per))) & ((1u << w) - 1u)) + *c;
+  *c = d >= (1 << (w-1)) && p < FD_KTAB_POS-1;
+  return d - (*c << w);
 }
 
 /* Verify with a cached key: the reference equation itself,
-   [S]B + [k](-A) == R (fd_ed25519_user.c:208-228), as 64 mixed additions
+   [S]B + [k](-A) == R (fd_ed25519_user.c:208-228), as FD_KTAB_POS mixed additions
    from the key's comb table plus 16 from the fixed-base comb table -- no
    doublings, no lattice, no decode of A, no per-signature tables -- then
    the projective compare against the decoded R.  Codes follow the same

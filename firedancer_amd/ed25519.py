@@ -229,7 +229,7 @@ class Ed25519Gpu:
         return out
 
     def keycache_reserve(self, capacity):
-        """Size the hot-key cache (64 KB of HBM per key per device); clears it."""
+        """Size the hot-key cache (512 KB of HBM per key per device); clears it."""
         r = self.lib.fd_ed25519_gpu_keycache_reserve(self.ctx, capacity)
         if r:
             raise GpuError("fd_ed25519_gpu_keycache_reserve: %s (%d)" % (strerror(r), r))

@@ -98,12 +98,12 @@ int fd_ed25519_gpu_host_unregister( fd_ed25519_gpu_t * ctx, void * p );
 
 /* Hot-key cache.  Solana traffic is dominated by a few thousand repeat
    signers (validators' vote authorities), so the context can keep, per
-   cached public key A, a comb table of [j](16^p (-A)) (64 KB of HBM per
-   key, built once).  A signature whose key is cached is verified as the
-   reference's own equation [S]B + [k](-A) == R with 80 table additions and
-   no doublings; the batch is split by key on the device, codes are
+   cached public key A, a comb table of [j](256^p (-A)), p < 32, j <= 128
+   (512 KB of HBM per key, built once).  A signature whose key is cached is
+   verified as the reference's own equation [S]B + [k](-A) == R with 48
+   table additions and no doublings; the batch is split by key on the device, codes are
    unchanged (bit-exact either way).  reserve sizes the cache (per device:
-   capacity x 64 KB + lists for max_batch signatures; clears it); add
+   capacity x 512 KB + lists for max_batch signatures; clears it); add
    inserts keys (32 B each; already-cached keys are skipped; stops when
    full) and returns how many were added. */
 int      fd_ed25519_gpu_keycache_reserve( fd_ed25519_gpu_t * ctx, uint64_t capacity );
