@@ -3,11 +3,14 @@
      fd_verify_offload_server [--name /fd_verify_offload] [--depth 262144]
                               [--dcache-mb 512] [--batch 65536] [--threads 4]
                               [--gpus 0x1] [--tcache-depth 16] [--tcache-map 64]
+                              [--hot-keys FILE [--hot-cap N]]
 
    Creates the shared-memory link, owns the GPU context and the verify tile's
    ha-dedup tcache (default depth 16 / map 64, fd_verify.h:6-7), serves until
    a client calls fd_verify_offload_halt (or SIGINT / SIGTERM), prints one
-   JSON line of stats and removes the link. */
+   JSON line of stats and removes the link.  --hot-keys: a file of 32-byte
+   public keys (e.g. the epoch's vote authorities) put in the hot-key cache
+   (fd_ed25519_gpu_keycache_*) before serving. */
 
 #include "../../include/fd_ed25519_gpu.h"
 #include "../../include/fd_verify_offload.h"
@@ -24,6 +27,7 @@ int main( int argc, char ** argv ) {
   char const * name = "/fd_verify_offload";
   uint64_t depth = 1ull << 18, dcache_mb = 512, batch = 65536, gpus = 1, tdepth = 16, tmap = 64;
   int threads = 4;
+  char const * hot = NULL; uint64_t hot_cap = 0;
   for( int i=1; i+1<argc; i+=2 ) {
     if     ( !strcmp( argv[i], "--name"         ) ) name      = argv[i+1];
     else if( !strcmp( argv[i], "--depth"        ) ) depth     = strtoull( argv[i+1], NULL, 0 );
@@ -33,6 +37,8 @@ int main( int argc, char ** argv ) {
     else if( !strcmp( argv[i], "--gpus"         ) ) gpus      = strtoull( argv[i+1], NULL, 0 );
     else if( !strcmp( argv[i], "--tcache-depth" ) ) tdepth    = strtoull( argv[i+1], NULL, 0 );
     else if( !strcmp( argv[i], "--tcache-map"   ) ) tmap      = strtoull( argv[i+1], NULL, 0 );
+    else if( !strcmp( argv[i], "--hot-keys"     ) ) hot       = argv[i+1];
+    else if( !strcmp( argv[i], "--hot-cap"      ) ) hot_cap   = strtoull( argv[i+1], NULL, 0 );
     else { fprintf( stderr, "unknown option %s\n", argv[i] ); return 2; }
   }
   fd_verify_offload_t * off = fd_verify_offload_create( name, depth, dcache_mb << 20 );
@@ -42,6 +48,21 @@ int main( int argc, char ** argv ) {
   fd_ed25519_gpu_t * ctx = fd_ed25519_gpu_new( gpus, batch * 4u );   /* larger batches are chunked internally */
   fd_ed25519_gpu_tcache_t * tc = fd_ed25519_gpu_tcache_new( tdepth, tmap );
   if( !ctx || !tc ) { fprintf( stderr, "GPU context / tcache creation failed\n" ); fd_verify_offload_unlink( name ); return 1; }
+  if( hot ) {
+    FILE * f = fopen( hot, "rb" );
+    if( !f ) { fprintf( stderr, "cannot open %s\n", hot ); fd_verify_offload_unlink( name ); return 1; }
+    fseek( f, 0, SEEK_END ); long fsz = ftell( f ); fseek( f, 0, SEEK_SET );
+    uint64_t nk = (uint64_t)(fsz > 0 ? fsz : 0) / 32u;
+    uint8_t * keys = (uint8_t *)malloc( nk * 32u + 1u );
+    if( !keys || fread( keys, 32u, nk, f ) != nk ) { fprintf( stderr, "read %s failed\n", hot ); fclose( f ); return 1; }
+    fclose( f );
+    if( !hot_cap ) hot_cap = nk;
+    int e = fd_ed25519_gpu_keycache_reserve( ctx, hot_cap );
+    int64_t added = e ? e : fd_ed25519_gpu_keycache_add( ctx, keys, nk );
+    free( keys );
+    if( added < 0 ) { fprintf( stderr, "hot-key cache: %s\n", fd_ed25519_gpu_strerror( (int)added ) ); fd_verify_offload_unlink( name ); return 1; }
+    fprintf( stderr, "fd_verify_offload_server: %ld hot keys cached\n", (long)added );
+  }
   uint8_t * dc = fd_verify_offload_dcache( off );
   int pinned = !fd_ed25519_gpu_host_register( ctx, dc, fd_verify_offload_dcache_sz( off ) );
   fprintf( stderr, "fd_verify_offload_server: frag area %s\n", pinned ? "page-locked" : "pageable (register failed)" );
