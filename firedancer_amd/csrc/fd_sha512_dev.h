@@ -56,7 +56,19 @@ FD_SHA_FN uint64_t sha_ror( uint64_t x, int n ) {
 
 /* Ch(e,f,g) = (e & f) ^ (~e & g) = bitfield insert; Maj(a,b,c) = (a^b) ? c : b. */
 FD_SHA_FN uint64_t sha_ch ( uint64_t e, uint64_t f, uint64_t g ) { return (e & f) | (~e & g); }
+#if defined(__HIP_DEVICE_COMPILE__)
+/* Maj as v_bfi_b32 per half (the compiler otherwise expands it to and/or) */
+FD_SHA_FN uint32_t sha_bfi( uint32_t m, uint32_t x, uint32_t y ) {
+  uint32_t r; asm( "v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y) ); return r;
+}
+FD_SHA_FN uint64_t sha_maj( uint64_t a, uint64_t b, uint64_t c ) {
+  uint64_t m = a ^ b;
+  return ((uint64_t)sha_bfi( (uint32_t)(m >> 32), (uint32_t)(c >> 32), (uint32_t)(b >> 32) ) << 32) |
+         sha_bfi( (uint32_t)m, (uint32_t)c, (uint32_t)b );
+}
+#else
 FD_SHA_FN uint64_t sha_maj( uint64_t a, uint64_t b, uint64_t c ) { uint64_t m = a ^ b; return (m & c) | (~m & b); }
+#endif
 
 FD_SHA_FN void sha512_init_state( uint64_t h[ 8 ] ) {
   h[0]=0x6a09e667f3bcc908ULL; h[1]=0xbb67ae8584caa73bULL; h[2]=0x3c6ef372fe94f82bULL; h[3]=0xa54ff53a5f1d36f1ULL;
