@@ -151,8 +151,8 @@ def main():
                          "4: the adversarial golden mix tiled to --batch per GPU")
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--hot-keys", type=int, default=0,
-                    help="config 2 with this many distinct signers, all in the hot-key cache "
-                         "(vote-like traffic; fd_ed25519_gpu_keycache_*)")
+                    help="config 2 / 3 with this many distinct signers, all in the hot-key cache "
+                         "(vote-like traffic; fd_ed25519_gpu_keycache_*, 512 KB of HBM per key)")
     ap.add_argument("--msg-sz", type=int, default=200)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -173,7 +173,8 @@ def main():
     if args.config == 3:
         total = args.batch or 1 << 20
         n = total // world + (1 if rank < total % world else 0)
-        arena, desc, sz, expect, data_desc = build_workload(n, None, seed=rank, n_keys=min(n, 65536))
+        arena, desc, sz, expect, data_desc = build_workload(n, None, seed=rank,
+                                                            n_keys=args.hot_keys or min(n, 65536))
     elif args.config == 4:
         n = args.batch or 65536
         arena, desc, sz, expect, data_desc = build_adversarial(n)
