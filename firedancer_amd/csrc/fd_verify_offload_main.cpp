@@ -71,10 +71,12 @@ int main( int argc, char ** argv ) {
   fflush( stderr );
   /* readiness marker for scripts: the link exists and the GPU is up */
   printf( "{\"ready\": true}\n" ); fflush( stdout );
-  uint64_t stats[ 4 ] = { 0, 0, 0, 0 };
+  uint64_t stats[ 7 ] = { 0, 0, 0, 0, 0, 0, 0 };
   int err = fd_verify_offload_serve( off, ctx, tc, batch, threads, stats );
-  printf( "{\"err\": %d, \"batches\": %lu, \"frags\": %lu, \"max_batch\": %lu, \"idle_polls\": %lu}\n", err,
-          (unsigned long)stats[0], (unsigned long)stats[1], (unsigned long)stats[2], (unsigned long)stats[3] );
+  printf( "{\"err\": %d, \"batches\": %lu, \"frags\": %lu, \"max_batch\": %lu, \"idle_polls\": %lu, "
+          "\"submit_ms\": %.3f, \"complete_ms\": %.3f, \"first_to_last_ms\": %.3f}\n", err,
+          (unsigned long)stats[0], (unsigned long)stats[1], (unsigned long)stats[2], (unsigned long)stats[3],
+          (double)stats[4] / 1e6, (double)stats[5] / 1e6, (double)stats[6] / 1e6 );
   if( pinned ) fd_ed25519_gpu_host_unregister( ctx, dc );
   fd_ed25519_gpu_tcache_delete( tc );
   fd_ed25519_gpu_delete( ctx );

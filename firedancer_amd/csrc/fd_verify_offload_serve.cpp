@@ -17,16 +17,23 @@
 
 #include <time.h>
 
+static inline uint64_t now_ns( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 extern "C" int
 fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,
-                         uint64_t max_batch, int threads, uint64_t * stats /* [4]: batches, frags, max batch, idle polls */ ) {
+                         uint64_t max_batch, int threads,
+                         uint64_t * stats /* [7]: batches, frags, max batch, idle polls, ns in submit, ns in
+                                             completing polls, ns first frag -> last result */ ) {
   if( !off || !ctx || !tc || !max_batch ) return FD_ED25519_GPU_ERR_ARG;
   fd_ed25519_gpu_stage_t * st = fd_ed25519_gpu_stage_new( ctx, tc, max_batch, threads );
   if( !st ) return FD_ED25519_GPU_ERR_OOM;
   uint64_t q_seq[ 2 ], q_cnt[ 2 ];   /* outstanding batches, oldest first */
   int q = 0;
   uint64_t done = fd_verify_offload_done_seq( off );
-  uint64_t s_batches = 0, s_frags = 0, s_max = 0, s_idle = 0;
+  uint64_t s_batches = 0, s_frags = 0, s_max = 0, s_idle = 0, s_sub_ns = 0, s_poll_ns = 0, t_first = 0, t_last = 0;
   int err = FD_ED25519_GPU_OK;
   uint8_t * dc = fd_verify_offload_dcache( off );
   uint64_t dsz = fd_verify_offload_dcache_sz( off );
@@ -37,10 +44,13 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
       uint64_t m = avail < max_batch ? avail : max_batch;
       fd_verify_offload_frag_t const * f = fd_verify_offload_frag_laddr( off, first );
       for( uint64_t j=1; j<m; j++ ) if( f[ j ].off < f[ j-1 ].off ) { m = j; break; }   /* frag-area wrap */
+      uint64_t t0 = now_ns();
+      if( !t_first ) t_first = t0;
       err = fd_ed25519_gpu_stage_submit( st, dc, dsz, (fd_ed25519_gpu_frag_t const *)f, m,
                                          fd_verify_offload_result_laddr( off, first ),
                                          fd_verify_offload_sig_laddr( off, first ) );
       if( err ) break;
+      s_sub_ns += now_ns() - t0;
       fd_verify_offload_take( off, m );
       q_seq[ q ] = first; q_cnt[ q ] = m; q++;
       s_batches++; s_frags += m; s_max = m > s_max ? m : s_max;
@@ -49,8 +59,11 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
     if( q ) {
       /* block on the GPU only when there is nothing else to do */
       uint64_t f2; int more = fd_verify_offload_avail( off, &f2 ) != 0;
+      uint64_t t0 = now_ns();
       int r = fd_ed25519_gpu_stage_poll( st, !progressed && !more );
       if( r == FD_ED25519_GPU_OK ) {
+        t_last = now_ns();
+        s_poll_ns += t_last - t0;
         done = q_seq[ 0 ] + q_cnt[ 0 ];
         fd_verify_offload_complete( off, done );
         q_seq[ 0 ] = q_seq[ 1 ]; q_cnt[ 0 ] = q_cnt[ 1 ]; q--;
@@ -65,6 +78,9 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
     }
   }
   fd_ed25519_gpu_stage_delete( st );
-  if( stats ) { stats[0] = s_batches; stats[1] = s_frags; stats[2] = s_max; stats[3] = s_idle; }
+  if( stats ) {
+    stats[0] = s_batches; stats[1] = s_frags; stats[2] = s_max; stats[3] = s_idle;
+    stats[4] = s_sub_ns; stats[5] = s_poll_ns; stats[6] = t_last - t_first;
+  }
   return err;
 }

@@ -272,7 +272,26 @@ struct fd_ed25519_gpu_stage {
 static void
 vs_parse_range( vs_batch * b, uint8_t const * arena, uint64_t arena_sz, fd_ed25519_gpu_frag_t const * frag,
                 uint64_t lo, uint64_t hi ) {
+  /* The per-frag reads (trailer -> fd_txn_t -> signature) are dependent
+     cache misses into a large frag area: prefetch the trailer and the
+     signature line 16 frags ahead, and the fd_txn_t 8 ahead (its address
+     needs the trailer, by then in cache). */
   for( uint64_t i=lo; i<hi; i++ ) {
+    if( i + 16u < hi ) {
+      fd_ed25519_gpu_frag_t f = frag[ i + 16u ];
+      if( (uint64_t)f.off + f.sz <= arena_sz && f.sz >= 2u ) {
+        __builtin_prefetch( arena + f.off + f.sz - 2u );
+        __builtin_prefetch( arena + f.off );
+      }
+    }
+    if( i + 8u < hi ) {
+      fd_ed25519_gpu_frag_t f = frag[ i + 8u ];
+      if( (uint64_t)f.off + f.sz <= arena_sz && f.sz >= 2u ) {
+        uint64_t psz = ld16( arena + f.off + f.sz - 2u );
+        uint64_t t = ((uintptr_t)(arena + f.off) + psz + 1u) & ~(uintptr_t)1;
+        if( t + TXN_HDR_SZ <= (uintptr_t)arena + arena_sz ) __builtin_prefetch( (void const *)t );
+      }
+    }
     uint32_t so = 0, po = 0, mo = 0, ms = 0, cnt = 0;
     int st = frag_parse( arena, arena_sz, frag[ i ], &b->tag[ i ], &so, &po, &mo, &ms, &cnt );
     b->result[ i ] = (int8_t)st;
@@ -348,32 +367,59 @@ vs_parse( vs_batch * b, uint8_t const * arena, uint64_t arena_sz, fd_ed25519_gpu
   b->code.resize( b->ndesc ? (size_t)b->ndesc : 1u );
 }
 
-/* In-order replay of fd_txn_verify's tcache steps (fd_verify.h:63-86) over a
-   batch whose GPU codes are in. */
+/* Fold the GPU codes of frags [lo, hi) into one verify code per frag with
+   fd_ed25519_verify_batch_single_msg's precedence (first phase-1 error,
+   else ERR_MSG, else SUCCESS); k0 = the first descriptor of frag lo.  The
+   code goes into result[i] for frags that had descriptors (status 0). */
 static void
-vs_replay( fd_ed25519_gpu_tcache_t * tc, vs_batch * b ) {
-  uint64_t k = 0;
-  for( uint64_t i=0; i<b->n; i++ ) {
-    b->sig[ i ] = 0u;
-    int st = b->result[ i ];
-    if( st == FD_TXN_VERIFY_BAD_FRAG ) continue;
-    int8_t vcode = FD_ED25519_ERR_SIG;
-    if( !st ) {
-      /* fold this frag's codes with fd_ed25519_verify_batch_single_msg's
-         precedence (first phase-1 error, else ERR_MSG, else SUCCESS) */
-      uint64_t cnt = b->cnt[ i ];
-      int8_t first = 0, any_msg = 0;
-      for( uint64_t j=0; j<cnt; j++ ) {
-        int8_t c = b->code[ k + j ];
-        if( c == FD_ED25519_ERR_MSG ) any_msg = 1;
-        else if( c != FD_ED25519_SUCCESS && !first ) first = c;
-      }
-      vcode = first ? first : (any_msg ? (int8_t)FD_ED25519_ERR_MSG : (int8_t)FD_ED25519_SUCCESS);
-      k += cnt;
+vs_fold_range( vs_batch * b, uint64_t lo, uint64_t hi, uint64_t k0 ) {
+  uint64_t k = k0;
+  for( uint64_t i=lo; i<hi; i++ ) {
+    if( b->result[ i ] ) continue;                       /* FAILED / BAD_FRAG: no descriptors */
+    uint64_t cnt = b->cnt[ i ];
+    int8_t first = 0, any_msg = 0;
+    for( uint64_t j=0; j<cnt; j++ ) {
+      int8_t c = b->code[ k + j ];
+      if( c == FD_ED25519_ERR_MSG ) any_msg = 1;
+      else if( c != FD_ED25519_SUCCESS && !first ) first = c;
     }
+    b->result[ i ] = first ? first : (any_msg ? (int8_t)FD_ED25519_ERR_MSG : (int8_t)FD_ED25519_SUCCESS);
+    /* result[i] now holds the frag's verify code (0 = all signatures good) */
+    k += cnt;
+  }
+}
+
+/* In-order replay of fd_txn_verify's tcache steps (fd_verify.h:63-86) over a
+   batch whose GPU codes are in: the per-frag folds run on the stage's
+   threads, then the tcache steps -- the only order-dependent part -- run
+   sequentially. */
+static void
+vs_replay( fd_ed25519_gpu_tcache_t * tc, vs_batch * b, int threads ) {
+  uint64_t n = b->n;
+  /* keep the pre-fold status of the frags that never had descriptors */
+  /* (FAILED frags fold to ERR_SIG below, BAD_FRAG stays BAD_FRAG) */
+  int nt = (n >= 16384u && threads > 1) ? threads : 1;
+  if( nt == 1 ) vs_fold_range( b, 0u, n, 0u );
+  else {
+    std::vector<uint64_t> part( (size_t)nt + 1u ), k0( (size_t)nt + 1u, 0u );
+    for( int t=0; t<=nt; t++ ) part[ t ] = n * (uint64_t)t / (uint64_t)nt;
+    for( int t=0; t<nt; t++ ) {
+      uint64_t c = 0;
+      for( uint64_t i=part[t]; i<part[t+1]; i++ ) c += b->cnt[ i ];
+      k0[ t+1 ] = k0[ t ] + c;
+    }
+    std::vector<std::thread> th;
+    for( int t=0; t<nt; t++ ) th.emplace_back( vs_fold_range, b, part[t], part[t+1], k0[t] );
+    for( auto & x : th ) x.join();
+  }
+  for( uint64_t i=0; i<n; i++ ) {
+    int8_t v = b->result[ i ];
     uint64_t tag = b->tag[ i ];
+    b->sig[ i ] = 0u;
+    if( v == FD_TXN_VERIFY_BAD_FRAG ) continue;
+    if( v == FD_TXN_VERIFY_FAILED ) v = FD_ED25519_ERR_SIG;   /* signature_cnt 0 or > 16 */
     if( fd_ed25519_gpu_tcache_query( tc, tag ) ) { b->result[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
-    if( vcode != FD_ED25519_SUCCESS )            { b->result[ i ] = FD_TXN_VERIFY_FAILED; continue; }
+    if( v != FD_ED25519_SUCCESS )                { b->result[ i ] = FD_TXN_VERIFY_FAILED; continue; }
     if( tc_insert( tc, tag ) )                   { b->result[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
     b->result[ i ] = FD_TXN_VERIFY_SUCCESS;
     b->sig[ i ] = tag;
@@ -442,7 +488,7 @@ fd_ed25519_gpu_stage_poll( fd_ed25519_gpu_stage_t * st, int block ) {
     vs_batch * nb = &st->b[ st->head ^ 1 ];
     if( nb->state == 1 ) { int err = vs_launch( st->ctx, nb ); if( err ) return err; }
   }
-  vs_replay( st->tc, b );
+  vs_replay( st->tc, b, st->threads );
   b->state = 0;
   st->pending--;
   st->head ^= 1;
@@ -466,6 +512,6 @@ fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * t
     int err = fd_ed25519_verify_batch_gpu( ctx, b.arena, b.arena_sz, b.desc.data(), (uint64_t)b.ndesc, b.code.data() );
     if( err ) return err;
   }
-  vs_replay( tc, &b );
+  vs_replay( tc, &b, 1 );
   return FD_ED25519_GPU_OK;
 }

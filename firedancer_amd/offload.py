@@ -165,7 +165,7 @@ class ServeThread:
     def __init__(self, link, gpu, tcache, max_batch=65536, threads=4):
         lib = load_lib()
         lib.fd_verify_offload_serve.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
-        self.stats = (ctypes.c_uint64 * 4)()
+        self.stats = (ctypes.c_uint64 * 7)()
         self.rc = None
 
         def run():

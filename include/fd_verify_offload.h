@@ -109,8 +109,9 @@ struct fd_ed25519_gpu_tcache;
 /* Serve `off` until fd_verify_offload_halt is seen and every published frag
    has its result: batches of up to max_batch frags through the asynchronous
    verify stage (two in flight, host parse on `threads` threads), results in
-   seq order.  stats (optional, 4 u64): batches, frags, largest batch, idle
-   polls.  Returns FD_ED25519_GPU_OK or the first GPU error. */
+   seq order.  stats (optional, 7 u64): batches, frags, largest batch, idle
+   polls, ns spent submitting (host parse), ns in completing polls (GPU wait
+   + replay), ns from the first submit to the last completion.  Returns FD_ED25519_GPU_OK or the first GPU error. */
 int fd_verify_offload_serve( fd_verify_offload_t * off, struct fd_ed25519_gpu * ctx,
                              struct fd_ed25519_gpu_tcache * tc, uint64_t max_batch, int threads,
                              uint64_t * stats );

@@ -4,7 +4,7 @@
 set -e
 mkdir -p gpurun_out
 NAME=/fdvo_e2e_$$
-timeout -k 10 300 ./firedancer_amd/fd_verify_offload_server --name $NAME --batch ${BATCH:-65536} --threads ${THREADS:-8} \
+timeout -k 10 300 ./firedancer_amd/fd_verify_offload_server --name $NAME --batch ${BATCH:-65536} --threads ${THREADS:-16} \
   > gpurun_out/offload_server.json 2> gpurun_out/offload_server.err &
 SRV=$!
 timeout -k 10 240 python3 tools/bench_offload.py --name $NAME ${CLIENT_ARGS} > gpurun_out/offload_client.json 2> gpurun_out/offload_client.err || { kill $SRV; wait $SRV; exit 1; }
