@@ -18,6 +18,6 @@ from .ed25519 import (  # noqa: F401
 )
 from .verify_stage import (  # noqa: F401
     FD_TXN_VERIFY_BAD_FRAG, FD_TXN_VERIFY_DEDUP, FD_TXN_VERIFY_FAILED, FD_TXN_VERIFY_SUCCESS, FRAG_DTYPE, TCache,
-    VerifyStage, frags_to_descs,
+    VerifyStage, AsyncStage, frags_to_descs,
 )
 from .offload import OffloadLink, ServeThread, load_offload_lib, server_path  # noqa: F401

@@ -78,6 +78,27 @@ struct kpart_args {
   uint32_t *                hit_slot;
   uint32_t *                miss_idx;
   uint32_t *                counts;    /* [0] hits, [1] misses (zeroed before launch) */
+  uint32_t const *          ncnt;      /* if set: the batch is desc[0, min(n, *ncnt)) */
+};
+
+/* Device-side frag parsing (verify stage, fd_verify_stage.cpp): the frags
+   [off, off+sz) index a copy of the arena span [span_lo, span_lo+span_sz). */
+struct fparse_args {
+  uint8_t const *                span;       /* device copy of arena[span_lo, span_lo + span_sz) */
+  uint64_t                       span_sz;
+  uint64_t                       span_lo;
+  uint32_t                       host_parity; /* (uintptr_t)host_arena & 1: the tile aligns host addresses */
+  uint64_t                       arena_sz;   /* the host arena's size (frags beyond it are BAD) */
+  fd_ed25519_gpu_frag_t const *  frag;
+  uint64_t                       n;
+  int8_t *                       status;     /* out: 0 / FD_TXN_VERIFY_FAILED / _BAD_FRAG, then the fold */
+  uint64_t *                     tag;        /* out */
+  uint32_t *                     cnt;        /* out: descriptors per frag, then (scan) their first index */
+  uint32_t *                     fld;        /* out: 4 per frag: sig, pub, msg offsets (span-relative), msg_sz */
+  uint32_t *                     total;      /* scan: descriptor count */
+  fd_ed25519_desc_t *            desc;       /* emit: descriptors */
+  uint64_t                       desc_cap;
+  int8_t const *                 code;       /* fold: per-descriptor codes */
 };
 
 /* Kernel symbols in the code object (extern "C"). */
@@ -88,6 +109,10 @@ struct kpart_args {
 #define FD_KERN_KBUILD   "fd_ed25519_ktab_build_kernel"
 #define FD_KERN_KPART    "fd_ed25519_kcache_part_kernel"
 #define FD_KERN_CACHED   "fd_ed25519_verify_cached_kernel"
+#define FD_KERN_FPARSE   "fd_frag_parse_kernel"
+#define FD_KERN_FSCAN    "fd_frag_scan_kernel"
+#define FD_KERN_FEMIT    "fd_frag_emit_kernel"
+#define FD_KERN_FFOLD    "fd_frag_fold_kernel"
 
 /* Seeded key hash shared by the host (slot assignment) and the device
    (lookup): splitmix64 of the key's first 8 bytes xor seed. */

@@ -599,7 +599,9 @@ fd_ed25519_ktab_build_kernel( uint32_t * ktab, uint32_t * kmeta, uint32_t const 
 extern "C" __global__ void __launch_bounds__( 256 )
 fd_ed25519_kcache_part_kernel( kpart_args a ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool valid = i < a.n;
+  uint64_t nn = a.ncnt ? min( a.n, (uint64_t)*a.ncnt ) : a.n;
+  if( (i & ~(uint64_t)63) >= nn ) return;
+  bool valid = i < nn;
   int64_t slot = -1;
   if( valid ) {
     fd_ed25519_desc_t d = a.desc[ i ];
@@ -750,6 +752,110 @@ fd_ed25519_verify_cached_kernel( verify_args args ) {
     if( run ) code = ge_eq_z1( acc, R ) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;   /* :225-228 */
   }
   if( valid ) args.out[ di ] = (int8_t)code;
+}
+
+/* ------------------------------------------------------------------ frag parsing */
+
+/* The verify tile's per-frag checks and field reads (fd_verify.c:92-115,
+   fd_verify.h:49-60) on the GPU, one frag per lane, over a device copy of
+   the batch's frag span; the same logic as frag_parse in fd_verify_stage.cpp
+   (the host form), with one difference: a signature / pubkey / message
+   region outside the copied span (impossible for fd_txn_parse output) is
+   BAD_FRAG here. */
+__device__ __forceinline__ uint32_t span_ld16( uint8_t const * p ) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_frag_parse_kernel( fparse_args a ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= a.n ) return;
+  fd_ed25519_gpu_frag_t f = a.frag[ i ];
+  int st = FD_TXN_VERIFY_BAD_FRAG;
+  uint64_t tag = 0u;
+  uint32_t cnt = 0u, so = 0u, po = 0u, mo = 0u, ms = 0u;
+  uint64_t off = f.off, sz = f.sz;
+  do {
+    if( off > a.arena_sz || sz > a.arena_sz - off || sz < 2u ) break;          /* fd_verify.c:94-96 */
+    if( off < a.span_lo || off + sz > a.span_lo + a.span_sz ) break;
+    uint64_t ro = off - a.span_lo;                                              /* span-relative */
+    uint64_t psz = span_ld16( a.span + ro + sz - 2u );                          /* :98 */
+    if( psz > 2086u ) break;                                                    /* :101-103 */
+    uint64_t t = ro + psz + ((a.host_parity + off + psz) & 1u);                  /* :108 align_up( addr, 2 ) */
+    if( t + 14u > a.span_sz ) break;
+    uint8_t const * txn = a.span + t;
+    if( span_ld16( txn + 12 ) >= psz ) break;                                   /* :112-115 */
+    uint64_t c = txn[1];
+    uint64_t s_ = ro + span_ld16( txn + 2 ), p_ = ro + span_ld16( txn + 10 ), m_ = span_ld16( txn + 4 );
+    if( s_ + 8u > a.span_sz ) break;
+    uint8_t const * sg = a.span + s_;
+#pragma unroll
+    for( int b=7; b>=0; b-- ) tag = (tag << 8) | sg[b];
+    if( m_ > psz ) break;
+    if( !c || c > 16u ) { st = FD_TXN_VERIFY_FAILED; break; }                  /* batch_sz 0 or > 16 -> ERR_SIG */
+    if( s_ + 64u*c > a.span_sz || p_ + 32u*c > a.span_sz ) break;
+    st = 0; cnt = (uint32_t)c; so = (uint32_t)s_; po = (uint32_t)p_; mo = (uint32_t)(ro + m_); ms = (uint32_t)(psz - m_);
+  } while( 0 );
+  a.status[ i ] = (int8_t)st; a.tag[ i ] = tag; a.cnt[ i ] = cnt;
+  uint32_t * fl = a.fld + 4u*i;
+  fl[0] = so; fl[1] = po; fl[2] = mo; fl[3] = ms;
+}
+
+/* Exclusive prefix sum of cnt[0, n) in place, total -> *a.total.  One
+   workgroup of 1024 threads: per-thread chunk sums, an LDS scan of the 1024
+   partials, then each thread rewrites its chunk. */
+extern "C" __global__ void __launch_bounds__( 1024 )
+fd_frag_scan_kernel( fparse_args a ) {
+  __shared__ uint32_t part[ 1024 ];
+  uint32_t t = threadIdx.x;
+  uint64_t per = (a.n + 1023u) / 1024u;
+  uint64_t lo = (uint64_t)t * per, hi = min( a.n, lo + per );
+  uint32_t sum = 0u;
+  for( uint64_t i=lo; i<hi; i++ ) sum += a.cnt[ i ];
+  part[ t ] = sum;
+  __syncthreads();
+  for( uint32_t o=1u; o<1024u; o<<=1 ) {
+    uint32_t v = t >= o ? part[ t - o ] : 0u;
+    __syncthreads();
+    part[ t ] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[ t ] - sum;                 /* exclusive */
+  for( uint64_t i=lo; i<hi; i++ ) { uint32_t c = a.cnt[ i ]; a.cnt[ i ] = run; run += c; }
+  if( t == 1023u ) *a.total = part[ 1023 ];
+}
+
+/* Descriptors of every frag at its scanned position (txn_idx = frag index). */
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_frag_emit_kernel( fparse_args a ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= a.n || a.status[ i ] ) return;
+  uint32_t const * fl = a.fld + 4u*i;
+  uint64_t at = a.cnt[ i ];
+  uint32_t c = (uint32_t)((i + 1u < a.n ? (uint64_t)a.cnt[ i + 1u ] : (uint64_t)*a.total) - at);
+  for( uint32_t j=0; j<c && at + j < a.desc_cap; j++ ) {
+    fd_ed25519_desc_t d;
+    d.sig_off = fl[0] + 64u*j; d.pub_off = fl[1] + 32u*j; d.msg_off = fl[2];
+    d.msg_sz = (uint16_t)fl[3]; d.txn_idx = (uint16_t)i;
+    a.desc[ at + j ] = d;
+  }
+}
+
+/* Each frag's verify code from its descriptors' codes, with
+   fd_ed25519_verify_batch_single_msg's precedence (first phase-1 error,
+   else ERR_MSG, else SUCCESS), into status[i] for frags that had
+   descriptors. */
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_frag_fold_kernel( fparse_args a ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= a.n || a.status[ i ] ) return;
+  uint64_t at = a.cnt[ i ];
+  uint64_t end = i + 1u < a.n ? (uint64_t)a.cnt[ i + 1u ] : (uint64_t)*a.total;
+  int first = 0, any_msg = 0;
+  for( uint64_t k=at; k<end; k++ ) {
+    int c = a.code[ k ];
+    if( c == FD_ED25519_ERR_MSG ) any_msg = 1;
+    else if( c != FD_ED25519_SUCCESS && !first ) first = c;
+  }
+  a.status[ i ] = (int8_t)(first ? first : (any_msg ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS));
 }
 
 /* Self-test kernel (tests only, fd_ed25519_gpu_test_lattice): the device

@@ -45,7 +45,8 @@ int main( int argc, char ** argv ) {
   if( !off ) { fprintf( stderr, "fd_verify_offload_create(%s) failed\n", name ); return 1; }
   g_off = off;
   signal( SIGINT, on_signal ); signal( SIGTERM, on_signal );
-  fd_ed25519_gpu_t * ctx = fd_ed25519_gpu_new( gpus, batch * 4u );   /* larger batches are chunked internally */
+  /* room for 16 descriptors per frag: the stage parses frags on the GPU */
+  fd_ed25519_gpu_t * ctx = fd_ed25519_gpu_new( gpus, batch * 16u );
   fd_ed25519_gpu_tcache_t * tc = fd_ed25519_gpu_tcache_new( tdepth, tmap );
   if( !ctx || !tc ) { fprintf( stderr, "GPU context / tcache creation failed\n" ); fd_verify_offload_unlink( name ); return 1; }
   if( hot ) {

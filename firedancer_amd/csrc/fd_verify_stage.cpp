@@ -243,14 +243,27 @@ fd_ed25519_gpu_frags_to_descs( uint8_t const * arena, uint64_t arena_sz,
 /* ---- the whole stage ---------------------------------------------------- */
 
 /* One batch of frags between parse and replay. */
+/* The device-parse form of a batch (fd_ed25519_gpu_host.cpp): frags parsed,
+   verified and folded on the GPU; status (fold code / FAILED / BAD_FRAG) and
+   tag per frag come back. */
+extern "C" int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                                            fd_ed25519_gpu_frag_t const * frag, uint64_t n, int8_t * status,
+                                            uint64_t * tag );
+extern "C" int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t * ctx, int block );
+extern "C" uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx );
+
 struct vs_batch {
-  int                            state;     /* 0 free, 1 parsed, 2 on the GPU, 3 GPU done / nothing to verify */
-  uint8_t const *                arena;     /* rebased: the span the descriptors touch */
-  uint64_t                       arena_sz;
-  uint64_t                       n;         /* frags */
-  int64_t                        ndesc;
-  int8_t *                       result;    /* caller's, n */
-  uint64_t *                     sig;       /* caller's, n */
+  int                            state = 0; /* 0 free, 1 parsed, 2 on the GPU, 3 GPU done / nothing to verify */
+  int                            devp  = 0; /* parsed on the GPU (fd_ed25519_gpu_frags_submit) */
+  uint8_t const *                harena = nullptr;   /* devp: the caller's arena and frags */
+  uint64_t                       harena_sz = 0;
+  fd_ed25519_gpu_frag_t const *  hfrag = nullptr;
+  uint8_t const *                arena = nullptr;   /* rebased: the span the descriptors touch */
+  uint64_t                       arena_sz = 0;
+  uint64_t                       n = 0;             /* frags */
+  int64_t                        ndesc = 0;
+  int8_t *                       result = nullptr;  /* caller's, n */
+  uint64_t *                     sig = nullptr;     /* caller's, n */
   std::vector<fd_ed25519_desc_t> desc;
   std::vector<uint64_t>          tag;
   std::vector<uint8_t>           cnt;
@@ -263,6 +276,7 @@ struct fd_ed25519_gpu_stage {
   fd_ed25519_gpu_tcache_t * tc;
   uint64_t                  max_frags;
   int                       threads;
+  int                       devparse;      /* parse frags on the GPU when the context has room */
   int                       head;          /* oldest pending slot */
   int                       pending;       /* 0..2 */
   vs_batch                  b[ 2 ];
@@ -396,10 +410,12 @@ vs_fold_range( vs_batch * b, uint64_t lo, uint64_t hi, uint64_t k0 ) {
 static void
 vs_replay( fd_ed25519_gpu_tcache_t * tc, vs_batch * b, int threads ) {
   uint64_t n = b->n;
+  if( b->devp ) threads = 0;              /* folded on the GPU already */
   /* keep the pre-fold status of the frags that never had descriptors */
   /* (FAILED frags fold to ERR_SIG below, BAD_FRAG stays BAD_FRAG) */
   int nt = (n >= 16384u && threads > 1) ? threads : 1;
-  if( nt == 1 ) vs_fold_range( b, 0u, n, 0u );
+  if( !threads ) {}
+  else if( nt == 1 ) vs_fold_range( b, 0u, n, 0u );
   else {
     std::vector<uint64_t> part( (size_t)nt + 1u ), k0( (size_t)nt + 1u, 0u );
     for( int t=0; t<=nt; t++ ) part[ t ] = n * (uint64_t)t / (uint64_t)nt;
@@ -427,7 +443,18 @@ vs_replay( fd_ed25519_gpu_tcache_t * tc, vs_batch * b, int threads ) {
 }
 
 static int
-vs_launch( fd_ed25519_gpu_t * ctx, vs_batch * b ) {
+vs_launch( fd_ed25519_gpu_t * ctx, vs_batch * b, int threads ) {
+  if( b->devp ) {
+    int err = fd_ed25519_gpu_frags_submit( ctx, b->harena, b->harena_sz, b->hfrag, b->n, b->result, b->tag.data() );
+    if( err != FD_ED25519_GPU_ERR_ARG ) {
+      if( err ) return err;
+      b->state = 2;
+      return FD_ED25519_GPU_OK;
+    }
+    /* the context has no room for 16 descriptors per frag: parse on the host */
+    b->devp = 0;
+    vs_parse( b, b->harena, b->harena_sz, b->hfrag, b->n, threads );
+  }
   if( !b->ndesc ) { b->state = 3; return FD_ED25519_GPU_OK; }
   int err = fd_ed25519_gpu_submit( ctx, b->arena, b->arena_sz, b->desc.data(), (uint64_t)b->ndesc, b->code.data() );
   if( err ) return err;
@@ -442,6 +469,7 @@ fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, 
   if( !st ) return NULL;
   st->ctx = ctx; st->tc = tc; st->max_frags = max_frags;
   st->threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+  st->devparse = 1;
   return st;
 }
 
@@ -460,10 +488,16 @@ fd_ed25519_gpu_stage_submit( fd_ed25519_gpu_stage_t * st, uint8_t const * arena,
   if( st->pending == 2 ) return FD_ED25519_GPU_ERR_BUSY;
   vs_batch * b = &st->b[ (st->head + st->pending) & 1 ];
   b->result = result; b->sig = sig;
-  vs_parse( b, arena, arena_sz, frag, frag_cnt, st->threads );
+  b->devp = st->devparse && frag_cnt && frag_cnt <= fd_ed25519_gpu_frags_cap( st->ctx );
+  if( b->devp ) {
+    b->n = frag_cnt; b->harena = arena; b->harena_sz = arena_sz; b->hfrag = frag; b->ndesc = 0;
+    b->tag.resize( frag_cnt );
+  } else {
+    vs_parse( b, arena, arena_sz, frag, frag_cnt, st->threads );
+  }
   b->state = 1;
   st->pending++;
-  if( st->pending == 1 ) return vs_launch( st->ctx, b );   /* the GPU is free: go */
+  if( st->pending == 1 ) return vs_launch( st->ctx, b, st->threads );   /* the GPU is free: go */
   return FD_ED25519_GPU_OK;                                  /* launched when the older batch's GPU work ends */
 }
 
@@ -472,10 +506,10 @@ fd_ed25519_gpu_stage_poll( fd_ed25519_gpu_stage_t * st, int block ) {
   if( !st ) return FD_ED25519_GPU_ERR_ARG;
   if( !st->pending ) return FD_ED25519_GPU_OK;
   vs_batch * b = &st->b[ st->head ];
-  if( b->state == 1 ) { int err = vs_launch( st->ctx, b ); if( err ) return err; }
+  if( b->state == 1 ) { int err = vs_launch( st->ctx, b, st->threads ); if( err ) return err; }
   if( b->state == 2 ) {
     for(;;) {
-      int r = fd_ed25519_gpu_poll( st->ctx );
+      int r = b->devp ? fd_ed25519_gpu_frags_poll( st->ctx, 0 ) : fd_ed25519_gpu_poll( st->ctx );
       if( r == FD_ED25519_GPU_OK ) break;
       if( r != FD_ED25519_GPU_PENDING ) { b->state = 0; st->pending--; st->head ^= 1; return r; }
       if( !block ) return FD_ED25519_GPU_PENDING;
@@ -486,7 +520,7 @@ fd_ed25519_gpu_stage_poll( fd_ed25519_gpu_stage_t * st, int block ) {
   /* the GPU is free: start the next batch before the host replays this one */
   if( st->pending == 2 ) {
     vs_batch * nb = &st->b[ st->head ^ 1 ];
-    if( nb->state == 1 ) { int err = vs_launch( st->ctx, nb ); if( err ) return err; }
+    if( nb->state == 1 ) { int err = vs_launch( st->ctx, nb, st->threads ); if( err ) return err; }
   }
   vs_replay( st->tc, b, st->threads );
   b->state = 0;
@@ -497,6 +531,13 @@ fd_ed25519_gpu_stage_poll( fd_ed25519_gpu_stage_t * st, int block ) {
 
 extern "C" int
 fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st ) { return st ? st->pending : 0; }
+
+extern "C" int
+fd_ed25519_gpu_stage_set_device_parse( fd_ed25519_gpu_stage_t * st, int on ) {
+  if( !st || st->pending ) return FD_ED25519_GPU_ERR_ARG;
+  st->devparse = !!on;
+  return FD_ED25519_GPU_OK;
+}
 
 extern "C" int
 fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,

@@ -103,3 +103,55 @@ class VerifyStage:
     def close(self):
         self.gpu.close()
         self.tcache.close()
+
+
+class AsyncStage:
+    """fd_ed25519_gpu_stage_*: two batches in flight, completed in order;
+    frags parsed on the GPU by default (device_parse=False: on the host)."""
+
+    def __init__(self, gpu, tcache, max_frags, threads=4, device_parse=True):
+        import ctypes as C
+        lib = load_lib()
+        vp = C.c_void_p
+        lib.fd_ed25519_gpu_stage_new.restype = vp
+        lib.fd_ed25519_gpu_stage_new.argtypes = [vp, vp, C.c_uint64, C.c_int]
+        lib.fd_ed25519_gpu_stage_submit.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp]
+        lib.fd_ed25519_gpu_stage_poll.argtypes = [vp, C.c_int]
+        lib.fd_ed25519_gpu_stage_pending.argtypes = [vp]
+        lib.fd_ed25519_gpu_stage_delete.argtypes = [vp]
+        lib.fd_ed25519_gpu_stage_set_device_parse.argtypes = [vp, C.c_int]
+        self.lib, self.gpu, self.tcache = lib, gpu, tcache
+        self.st = lib.fd_ed25519_gpu_stage_new(gpu.ctx, tcache.tc, max_frags, threads)
+        if not self.st:
+            raise GpuError("fd_ed25519_gpu_stage_new failed")
+        lib.fd_ed25519_gpu_stage_set_device_parse(self.st, 1 if device_parse else 0)
+        self._keep = []
+
+    def submit(self, arena, arena_sz, frags, result, sig):
+        """Enqueue a batch (arrays must stay alive until its poll returns 0)."""
+        r = self.lib.fd_ed25519_gpu_stage_submit(self.st, _ptr(arena), arena_sz, _ptr(frags), len(frags),
+                                                 _ptr(result), _ptr(sig))
+        if r == -104:
+            return False
+        if r:
+            raise GpuError("fd_ed25519_gpu_stage_submit: %s (%d)" % (strerror(r), r))
+        self._keep.append((arena, frags, result, sig))
+        return True
+
+    def poll(self, block=True):
+        r = self.lib.fd_ed25519_gpu_stage_poll(self.st, 1 if block else 0)
+        if r == 1:
+            return False
+        if r:
+            raise GpuError("fd_ed25519_gpu_stage_poll: %s (%d)" % (strerror(r), r))
+        if self._keep:
+            self._keep.pop(0)
+        return True
+
+    def pending(self):
+        return int(self.lib.fd_ed25519_gpu_stage_pending(self.st))
+
+    def close(self):
+        if self.st:
+            self.lib.fd_ed25519_gpu_stage_delete(self.st)
+            self.st = None

@@ -259,6 +259,15 @@ int  fd_ed25519_gpu_stage_submit ( fd_ed25519_gpu_stage_t * st, uint8_t const * 
                                    int8_t * result, uint64_t * sig );
 int  fd_ed25519_gpu_stage_poll   ( fd_ed25519_gpu_stage_t * st, int block );
 int  fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st );
+/* By default the stage parses frags on the GPU (the frags' arena span is
+   copied to HBM; parse, descriptor emission, verify and the per-frag fold
+   run there; the host only replays the tcache), falling back to the host
+   parse when the context's max_batch is below 16 x frags per device.  One
+   difference from the host parse: a frag whose fd_txn_t places signatures /
+   pubkeys / message outside the batch's frag span (impossible for
+   fd_txn_parse output) is BAD_FRAG on the GPU.  on = 0 selects the host
+   parse (no batches may be pending). */
+int  fd_ed25519_gpu_stage_set_device_parse( fd_ed25519_gpu_stage_t * st, int on );
 
 /* ---- Ed25519 precompile instructions ----------
 

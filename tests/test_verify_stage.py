@@ -320,10 +320,12 @@ def test_verify_frags_random_stream_vs_reference_tile(gpu, ref):
 
 
 @pytest.mark.gpu
-def test_stage_async_two_in_flight_vs_reference_tile(gpu, ref):
+@pytest.mark.parametrize("devparse", [1, 0])
+def test_stage_async_two_in_flight_vs_reference_tile(gpu, ref, devparse):
     """The asynchronous stage (fd_ed25519_gpu_stage_*): batches of varying
     size submitted with up to two outstanding, completed in order; results
-    equal the sequential reference tile's."""
+    equal the sequential reference tile's -- with the frags parsed on the GPU
+    (default) and on the host."""
     import ctypes as C
     rng = np.random.default_rng(77)
     arena, frags = _random_frag_stream(rng, 1500, 4000)
@@ -339,6 +341,8 @@ def test_stage_async_two_in_flight_vs_reference_tile(gpu, ref):
     tc = fa.TCache()
     st = lib.fd_ed25519_gpu_stage_new(gpu.ctx, tc.tc, 4096, 4)
     assert st
+    lib.fd_ed25519_gpu_stage_set_device_parse.argtypes = [vp, C.c_int]
+    assert lib.fd_ed25519_gpu_stage_set_device_parse(st, devparse) == 0
     res = np.zeros(len(frags), np.int8)
     sig = np.zeros(len(frags), np.uint64)
     fr = np.ascontiguousarray(frags)

@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--async-batch", type=int, default=16384)
     args = ap.parse_args()
     import firedancer_amd as fa
 
@@ -93,6 +94,30 @@ def main():
         stage.verify_frags(arena, len(arena), frags)
         times.append(time.perf_counter() - t1)
     dt = float(np.mean(times))
+    # the asynchronous stage with the frags parsed on the GPU: --async-batch
+    # frags per batch, two batches in flight, over the same stream
+    ab = args.async_batch
+    big = fa.Ed25519Gpu(device_mask=1, max_batch=16 * ab)
+    ast = fa.AsyncStage(big, fa.TCache(), ab, threads=8, device_parse=True)
+    res_a = np.zeros(len(frags), np.int8); sig_a = np.zeros(len(frags), np.uint64)
+    fr = np.ascontiguousarray(frags)
+
+    def run_async():
+        ast.tcache.reset()
+        i = 0
+        while i < len(fr) or ast.pending():
+            if i < len(fr) and ast.pending() < 2:
+                j = min(len(fr), i + ab)
+                ast.submit(arena, len(arena), fr[i:j], res_a[i:j], sig_a[i:j])
+                i = j
+            else:
+                ast.poll(True)
+    run_async()
+    t_a = []
+    for _ in range(args.steps):
+        t1 = time.perf_counter(); run_async(); t_a.append(time.perf_counter() - t1)
+    dt_a = float(np.mean(t_a))
+    ast.close(); big.close()
     line = {"metric": "verify-stage frags/sec (fd_ed25519_gpu_verify_frags, host frags)",
             "value": args.frags / dt, "unit": "frags/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt * 1e3, "higher_is_better": True, "dtype": "u32 limbs / u8 bytes",
@@ -100,6 +125,8 @@ def main():
             "config": {"workload": "%d frags, %d signatures, tcache depth 16 / map 64" % (args.frags, n_sigs),
                        "arena_bytes": int(len(arena))},
             "sigs_per_s": n_sigs / dt, "host_parse_ms": parse_ms, "results": hist, "gen_s": gen_s,
+            "async_device_parse": {"frags_per_s": args.frags / dt_a, "ms": dt_a * 1e3, "batch": ab,
+                                   "results": {int(k): int(v) for k, v in zip(*np.unique(res_a, return_counts=True))}},
             "cpu_baseline": None if args.no_cpu else cpu_baseline(arena, frags)}
     print(json.dumps(line), flush=True)
     stage.close()
