@@ -446,6 +446,7 @@ static int
 vs_launch( fd_ed25519_gpu_t * ctx, vs_batch * b, int threads ) {
   if( b->devp ) {
     int err = fd_ed25519_gpu_frags_submit( ctx, b->harena, b->harena_sz, b->hfrag, b->n, b->result, b->tag.data() );
+    if( err == FD_ED25519_GPU_ERR_BUSY ) return err;   /* both frag slots queued: stays parsed (state 1) */
     if( err != FD_ED25519_GPU_ERR_ARG ) {
       if( err ) return err;
       b->state = 2;
@@ -498,7 +499,16 @@ fd_ed25519_gpu_stage_submit( fd_ed25519_gpu_stage_t * st, uint8_t const * arena,
   b->state = 1;
   st->pending++;
   if( st->pending == 1 ) return vs_launch( st->ctx, b, st->threads );   /* the GPU is free: go */
-  return FD_ED25519_GPU_OK;                                  /* launched when the older batch's GPU work ends */
+  /* Two device-parsed batches can both be queued: this one's frag span goes
+     to HBM on its own copy stream while the older one's kernels run (its
+     kernels follow them in order).  Otherwise it is launched when the
+     older batch's GPU work ends. */
+  vs_batch * ob = &st->b[ st->head ];
+  if( b->devp && ob->devp && ob->state >= 2 ) {
+    int err = vs_launch( st->ctx, b, st->threads );
+    return err == FD_ED25519_GPU_ERR_BUSY ? FD_ED25519_GPU_OK : err;
+  }
+  return FD_ED25519_GPU_OK;
 }
 
 extern "C" int

@@ -194,6 +194,18 @@ class Ed25519Gpu:
             raise GpuError("fd_ed25519_gpu_poll: %s (%d)" % (strerror(r), r))
         return r == GPU_OK
 
+    def host_register(self, buf):
+        """Page-lock a host array (e.g. a frag area) for every device of the context
+        (fd_ed25519_gpu_host_register): its per-batch copies to HBM become direct DMA."""
+        r = self.lib.fd_ed25519_gpu_host_register(self.ctx, _ptr(buf), buf.nbytes)
+        if r:
+            raise GpuError("fd_ed25519_gpu_host_register: %s (%d)" % (strerror(r), r))
+
+    def host_unregister(self, buf):
+        r = self.lib.fd_ed25519_gpu_host_unregister(self.ctx, _ptr(buf))
+        if r:
+            raise GpuError("fd_ed25519_gpu_host_unregister: %s (%d)" % (strerror(r), r))
+
     def verify_batch_dev(self, d_arena, arena_sz, d_desc, desc_cnt, d_out, stream=0, dev_idx=0):
         """Device pointers (ints), enqueue only."""
         r = self.lib.fd_ed25519_verify_batch_gpu_dev(self.ctx, dev_idx, d_arena, arena_sz, d_desc, desc_cnt,

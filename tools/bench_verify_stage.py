@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--async-batch", type=int, default=16384)
+    ap.add_argument("--async-batch", type=int, default=32768)
     args = ap.parse_args()
     import firedancer_amd as fa
 
@@ -112,11 +112,20 @@ def main():
                 i = j
             else:
                 ast.poll(True)
-    run_async()
-    t_a = []
-    for _ in range(args.steps):
-        t1 = time.perf_counter(); run_async(); t_a.append(time.perf_counter() - t1)
-    dt_a = float(np.mean(t_a))
+    def timed():
+        run_async()
+        t = []
+        for _ in range(args.steps):
+            t1 = time.perf_counter(); run_async(); t.append(time.perf_counter() - t1)
+        return float(np.mean(t))
+    dt_a = timed()
+    res_pageable = res_a.copy()
+    # the same with the frag area page-locked (a tile's dcache workspace is
+    # registered once: fd_ed25519_gpu_host_register)
+    big.host_register(arena)
+    dt_r = timed()
+    big.host_unregister(arena)
+    assert np.array_equal(res_a, res_pageable)
     ast.close(); big.close()
     line = {"metric": "verify-stage frags/sec (fd_ed25519_gpu_verify_frags, host frags)",
             "value": args.frags / dt, "unit": "frags/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -126,6 +135,7 @@ def main():
                        "arena_bytes": int(len(arena))},
             "sigs_per_s": n_sigs / dt, "host_parse_ms": parse_ms, "results": hist, "gen_s": gen_s,
             "async_device_parse": {"frags_per_s": args.frags / dt_a, "ms": dt_a * 1e3, "batch": ab,
+                                   "registered_frags_per_s": args.frags / dt_r, "registered_ms": dt_r * 1e3,
                                    "results": {int(k): int(v) for k, v in zip(*np.unique(res_a, return_counts=True))}},
             "cpu_baseline": None if args.no_cpu else cpu_baseline(arena, frags)}
     print(json.dumps(line), flush=True)
