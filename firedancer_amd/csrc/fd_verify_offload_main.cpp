@@ -70,6 +70,12 @@ int main( int argc, char ** argv ) {
   fprintf( stderr, "fd_verify_offload_server: serving %s (depth %lu, frag area %lu MB, batch %lu)\n",
            name, (unsigned long)depth, (unsigned long)dcache_mb, (unsigned long)batch );
   fflush( stderr );
+  /* size and warm the stage's device-parse path (first copies / launches)
+     before declaring readiness; serve's own stage then starts warm */
+  {
+    fd_ed25519_gpu_stage_t * ws = fd_ed25519_gpu_stage_new( ctx, tc, batch, threads );
+    if( ws ) { fd_ed25519_gpu_stage_warm( ws, dc, fd_verify_offload_dcache_sz( off ) ); fd_ed25519_gpu_stage_delete( ws ); }
+  }
   /* readiness marker for scripts: the link exists and the GPU is up */
   printf( "{\"ready\": true}\n" ); fflush( stdout );
   uint64_t stats[ 7 ] = { 0, 0, 0, 0, 0, 0, 0 };

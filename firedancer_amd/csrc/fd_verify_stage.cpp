@@ -251,6 +251,7 @@ extern "C" int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t * ctx, uint8_t cons
                                             uint64_t * tag );
 extern "C" int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t * ctx, int block );
 extern "C" uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx );
+extern "C" int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n );
 
 struct vs_batch {
   int                            state = 0; /* 0 free, 1 parsed, 2 on the GPU, 3 GPU done / nothing to verify */
@@ -471,7 +472,31 @@ fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, 
   st->ctx = ctx; st->tc = tc; st->max_frags = max_frags;
   st->threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
   st->devparse = 1;
+  /* size the device-parse buffers now, not while a batch is in flight
+     (best effort: a context too small for max_frags parses on the host) */
+  if( max_frags <= fd_ed25519_gpu_frags_cap( ctx ) ) fd_ed25519_gpu_frags_reserve( ctx, max_frags );
   return st;
+}
+
+extern "C" int
+fd_ed25519_gpu_stage_warm( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, uint64_t arena_sz ) {
+  if( !st || st->pending || (!arena && arena_sz) ) return FD_ED25519_GPU_ERR_ARG;
+  uint64_t n = st->max_frags;
+  if( !st->devparse || n > fd_ed25519_gpu_frags_cap( st->ctx ) ) return FD_ED25519_GPU_OK;
+  static uint8_t const zero[ 64 ] = { 0 };
+  if( !arena_sz ) { arena = zero; arena_sz = sizeof(zero); }
+  /* full-size throw-away batches of one repeated short frag (it fails the
+     frag checks: no descriptors) through both slots */
+  std::vector<fd_ed25519_gpu_frag_t> fr( n );
+  for( uint64_t i=0; i<n; i++ ) { fr[ i ].off = 0u; fr[ i ].sz = (uint32_t)(arena_sz < 64u ? arena_sz : 64u); }
+  std::vector<int8_t> status( 2u * n ); std::vector<uint64_t> tag( 2u * n );
+  int err = FD_ED25519_GPU_OK, queued = 0;
+  for( int k=0; k<2 && !err; k++ ) {
+    err = fd_ed25519_gpu_frags_submit( st->ctx, arena, arena_sz, fr.data(), n, status.data() + k * n, tag.data() + k * n );
+    queued += !err;
+  }
+  while( queued-- ) { int r = fd_ed25519_gpu_frags_poll( st->ctx, 1 ); if( !err ) err = r; }
+  return err;
 }
 
 extern "C" void

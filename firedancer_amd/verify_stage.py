@@ -120,6 +120,7 @@ class AsyncStage:
         lib.fd_ed25519_gpu_stage_pending.argtypes = [vp]
         lib.fd_ed25519_gpu_stage_delete.argtypes = [vp]
         lib.fd_ed25519_gpu_stage_set_device_parse.argtypes = [vp, C.c_int]
+        lib.fd_ed25519_gpu_stage_warm.argtypes = [vp, vp, C.c_uint64]
         self.lib, self.gpu, self.tcache = lib, gpu, tcache
         self.st = lib.fd_ed25519_gpu_stage_new(gpu.ctx, tcache.tc, max_frags, threads)
         if not self.st:
@@ -150,6 +151,14 @@ class AsyncStage:
 
     def pending(self):
         return int(self.lib.fd_ed25519_gpu_stage_pending(self.st))
+
+    def warm(self, arena=None):
+        """fd_ed25519_gpu_stage_warm: pay first-use costs (first DMA from a registered
+        frag area, first launches) before live traffic."""
+        r = self.lib.fd_ed25519_gpu_stage_warm(self.st, None if arena is None else _ptr(arena),
+                                               0 if arena is None else arena.nbytes)
+        if r:
+            raise GpuError("fd_ed25519_gpu_stage_warm: %s (%d)" % (strerror(r), r))
 
     def close(self):
         if self.st:

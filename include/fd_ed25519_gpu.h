@@ -269,6 +269,14 @@ int  fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st );
    parse (no batches may be pending). */
 int  fd_ed25519_gpu_stage_set_device_parse( fd_ed25519_gpu_stage_t * st, int on );
 
+/* Runs throw-away full-size batches (one short frag at the start of arena,
+   repeated; no signatures) through the device-parse path, so first-use
+   costs -- the first DMA from a newly registered frag area, first launches
+   -- are paid at init (the tile's privileged_init / the offload server
+   before it reports ready), not by live traffic.  arena may be NULL with
+   arena_sz 0.  No frags may be pending; the tcache is not touched. */
+int  fd_ed25519_gpu_stage_warm( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, uint64_t arena_sz );
+
 /* ---- Ed25519 precompile instructions ----------
 
    Batched form of fd_ed25519_program_execute

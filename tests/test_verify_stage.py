@@ -343,6 +343,9 @@ def test_stage_async_two_in_flight_vs_reference_tile(gpu, ref, devparse):
     assert st
     lib.fd_ed25519_gpu_stage_set_device_parse.argtypes = [vp, C.c_int]
     assert lib.fd_ed25519_gpu_stage_set_device_parse(st, devparse) == 0
+    # throw-away warm-up batches over this arena: must leave the tcache and results alone
+    lib.fd_ed25519_gpu_stage_warm.argtypes = [vp, vp, C.c_uint64]
+    assert lib.fd_ed25519_gpu_stage_warm(st, _vp(arena), len(arena)) == 0
     res = np.zeros(len(frags), np.int8)
     sig = np.zeros(len(frags), np.uint64)
     fr = np.ascontiguousarray(frags)
