@@ -165,10 +165,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+
+    def barrier():
+        if world > 1:
+            if dist.get_backend() == "nccl":
+                dist.barrier(device_ids=[local])
+            else:
+                dist.barrier()
 
     if args.config == 3:
         total = args.batch or 1 << 20
@@ -204,8 +211,7 @@ def main():
     assert np.array_equal(d_out.cpu().numpy(), expect), "verify codes differ from the expected ones"
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -213,8 +219,7 @@ def main():
         step()
         ev[i][1].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     dt = time.perf_counter() - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     assert np.array_equal(d_out.cpu().numpy(), expect)
