@@ -103,6 +103,7 @@ struct fparse_args {
 
 /* Kernel symbols in the code object (extern "C"). */
 #define FD_KERN_VERIFY   "fd_ed25519_verify_kernel"
+#define FD_KERN_VPAIR    "fd_ed25519_verify_pair_kernel"
 #define FD_KERN_CTAB     "fd_ed25519_ctab_init"
 #define FD_KERN_LATTEST  "fd_ed25519_lattice_test_kernel"
 #define FD_KERN_SHA512   "fd_sha512_batch_kernel"

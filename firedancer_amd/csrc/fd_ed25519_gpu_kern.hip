@@ -29,7 +29,7 @@
    build compiles none of it. */
 #ifdef FD_PHASE_STAMPS
 #define FD_NSTAMP 8
-#define STAMP( i ) do { FE_FENCE(); _st[ i ] = __builtin_amdgcn_s_memtime(); FE_FENCE(); } while( 0 )
+#define STAMP( i ) do { FE_FENCE(); if( _st ) _st[ i ] = __builtin_amdgcn_s_memtime(); FE_FENCE(); } while( 0 )
 #else
 #define STAMP( i ) do {} while( 0 )
 #endif
@@ -333,6 +333,97 @@ __device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 
   }
 }
 
+/* k = SHA-512(R||A||M) mod l, the lattice vector (u, v), w = v S mod l, and
+   their digits into this lane's LDS column drow (rows FD_ROW_U / _V / _W;
+   FD_ROW_NW of lane 0: the wave-uniform window count).  Lanes that are not
+   live write zero digits (every lane takes part in the wave max). */
+__device__ __forceinline__ void verify_prep_digits( uint8_t * drow, int tid, bool live, uint32_t const sig[ 16 ],
+                                                    uint32_t const pub[ 8 ], verify_args const & args,
+                                                    fd_ed25519_desc_t const & d, uint32_t lim_dw
+#ifdef FD_PHASE_STAMPS
+                                                    , uint64_t * _st
+#endif
+                                                    ) {
+  uint32_t u[ 8 ], v[ 8 ];
+  int un = 0, nbits = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; }
+  if( live ) {
+    uint32_t k[ 8 ];
+    hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );  /* :203-206 */
+    FE_FENCE();
+    STAMP( 2 );
+    lat_short_vector( k, u, v, &un );
+    FE_FENCE();
+    uint32_t pr[ 16 ];                                                 /* w = v S mod l */
+#pragma unroll
+    for( int j=0; j<16; j++ ) pr[j] = 0u;
+#pragma unroll
+    for( int i=0; i<8; i++ ) {
+      uint64_t c = 0;
+#pragma unroll
+      for( int j=0; j<8; j++ ) { uint64_t t = (uint64_t)v[i] * sig[8+j] + pr[i+j] + c; pr[i+j] = (uint32_t)t; c = t >> 32; }
+      pr[i+8] = (uint32_t)c;
+    }
+    uint32_t w[ 8 ];
+    sc_reduce512( w, pr );
+    /* signed 16-bit windows: d_k in [-2^15, 2^15), the top one (w < 2^253)
+       keeps its carry: d_15 <= 2^13 */
+    int c = 0;
+#pragma unroll
+    for( int k=0; k<FD_CTAB_POS; k++ ) {
+      int dd = (int)((w[k>>1] >> (16*(k&1))) & 0xffffu) + c;
+      c = dd >= 32768 && k < FD_CTAB_POS-1;
+      dd -= c << 16;
+      drow[ (FD_ROW_W + 2*k    )*FD_VERIFY_BLOCK ] = (uint8_t)(dd & 255);
+      drow[ (FD_ROW_W + 2*k + 1)*FD_VERIFY_BLOCK ] = (uint8_t)((dd >> 8) & 255);
+    }
+    nbits = max( bitlen8( u ), bitlen8( v ) );
+  }
+  /* wave-uniform window count: x < 2^(4 nw - 1) for every lane's u, v */
+#pragma unroll
+  for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
+  int nw = min( FD_NDIG_MAX, max( 32, (nbits + 4) >> 2 ) );
+  recode4_lds( drow + FD_ROW_U*FD_VERIFY_BLOCK, u, un, nw );
+  recode4_lds( drow + FD_ROW_V*FD_VERIFY_BLOCK, v, 0,  nw );
+  if( (tid & 63) == 0 ) drow[ FD_ROW_NW*FD_VERIFY_BLOCK ] = (uint8_t)nw;
+  }
+
+/* The verify code from the check results, in the reference's order
+   (fd_ed25519_user.c:157-228), and for lanes still at 0 the equation:
+   Q = [u](-A) + [v](-R) + [w]B (tables at vtab[gid] / vtab[cap/2 + gid],
+   digits in LDS) and Q == O. */
+__device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_ok, bool bad_s, int stA, int stR,
+                                            uint8_t const * drow, uint8_t const * s_dig, int tid, uint64_t gid
+#ifdef FD_PHASE_STAMPS
+                                            , uint64_t * _st
+#endif
+                                            ) {
+  uint64_t cap = args.vtab_cap;
+  int code;
+  if     ( !desc_ok    ) code = FD_ED25519_GPU_CODE_BAD_DESC;
+  else if( bad_s       ) code = FD_ED25519_ERR_SIG;
+  else if( !(stA & 1)  ) code = args.ref_codes ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;   /* :190-192 */
+  else if( !(stR & 1)  ) code = FD_ED25519_ERR_SIG;
+  else if( stA & 2     ) code = FD_ED25519_ERR_PUBKEY;                                        /* :193-195 */
+  else if( stR & 2     ) code = FD_ED25519_ERR_SIG;                                           /* :196-198 */
+  else                   code = 0;
+
+  if( code == 0 ) {
+    int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
+    ge_p3 acc;
+    dsm_loop( acc, args.vtab, cap, gid, cap/2u + gid, drow, args.ctab, nw );
+    STAMP( 5 );
+    /* Q == O  <=>  X == 0 and Y == Z (the reference's projective compare, :225-228, on [v]D) */
+    fe dl;
+    int ex = fe_is_zero( acc.X );
+    fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
+    int ey = fe_is_zero( dl );
+    code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  }
+  return code;
+}
+
 /* One signature per lane:
      S check -> k = SHA-512(R||A||M) mod l -> (u, v) short vector of k mod 8l,
      w = v S mod l, digits -> LDS -> decode A and R, small-order checks,
@@ -383,51 +474,11 @@ fd_ed25519_verify_kernel( verify_args args ) {
 
   /* k, lattice vector, w and digits (before the decodes: only digits stay live) */
   uint8_t * drow = s_dig + tid;
-  {
-    uint32_t u[ 8 ], v[ 8 ];
-    int un = 0, nbits = 0;
-#pragma unroll
-    for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; }
-    if( live ) {
-      uint32_t k[ 8 ];
-      hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );  /* :203-206 */
-      FE_FENCE();
-      STAMP( 2 );
-      lat_short_vector( k, u, v, &un );
-      FE_FENCE();
-      uint32_t pr[ 16 ];                                                 /* w = v S mod l */
-#pragma unroll
-      for( int j=0; j<16; j++ ) pr[j] = 0u;
-#pragma unroll
-      for( int i=0; i<8; i++ ) {
-        uint64_t c = 0;
-#pragma unroll
-        for( int j=0; j<8; j++ ) { uint64_t t = (uint64_t)v[i] * sig[8+j] + pr[i+j] + c; pr[i+j] = (uint32_t)t; c = t >> 32; }
-        pr[i+8] = (uint32_t)c;
-      }
-      uint32_t w[ 8 ];
-      sc_reduce512( w, pr );
-      /* signed 16-bit windows: d_k in [-2^15, 2^15), the top one (w < 2^253)
-         keeps its carry: d_15 <= 2^13 */
-      int c = 0;
-#pragma unroll
-      for( int k=0; k<FD_CTAB_POS; k++ ) {
-        int dd = (int)((w[k>>1] >> (16*(k&1))) & 0xffffu) + c;
-        c = dd >= 32768 && k < FD_CTAB_POS-1;
-        dd -= c << 16;
-        drow[ (FD_ROW_W + 2*k    )*FD_VERIFY_BLOCK ] = (uint8_t)(dd & 255);
-        drow[ (FD_ROW_W + 2*k + 1)*FD_VERIFY_BLOCK ] = (uint8_t)((dd >> 8) & 255);
-      }
-      nbits = max( bitlen8( u ), bitlen8( v ) );
-    }
-    /* wave-uniform window count: x < 2^(4 nw - 1) for every lane's u, v */
-#pragma unroll
-    for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
-    int nw = min( FD_NDIG_MAX, max( 32, (nbits + 4) >> 2 ) );
-    recode4_lds( drow + FD_ROW_U*FD_VERIFY_BLOCK, u, un, nw );
-    recode4_lds( drow + FD_ROW_V*FD_VERIFY_BLOCK, v, 0,  nw );
-    if( (tid & 63) == 0 ) drow[ FD_ROW_NW*FD_VERIFY_BLOCK ] = (uint8_t)nw;
-  }
+  verify_prep_digits( drow, tid, live, sig, pub, args, d, lim_dw
+#ifdef FD_PHASE_STAMPS
+                      , _st
+#endif
+                      );
   FE_FENCE();
 
   /* decode A then R (:162 frombytes_2x), small order (:193-198), tables */
@@ -453,27 +504,11 @@ fd_ed25519_verify_kernel( verify_args args ) {
   STAMP( 4 );
 
   if( !valid ) return;
-  int code;
-  if     ( !desc_ok    ) code = FD_ED25519_GPU_CODE_BAD_DESC;
-  else if( bad_s       ) code = FD_ED25519_ERR_SIG;
-  else if( !(stA & 1)  ) code = args.ref_codes ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;   /* :190-192 */
-  else if( !(stR & 1)  ) code = FD_ED25519_ERR_SIG;
-  else if( stA & 2     ) code = FD_ED25519_ERR_PUBKEY;                                        /* :193-195 */
-  else if( stR & 2     ) code = FD_ED25519_ERR_SIG;                                           /* :196-198 */
-  else                   code = 0;
-
-  if( code == 0 ) {
-    int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
-    ge_p3 acc;
-    dsm_loop( acc, args.vtab, cap, gid, cap/2u + gid, drow, args.ctab, nw );
-    STAMP( 5 );
-    /* Q == O  <=>  X == 0 and Y == Z (the reference's projective compare, :225-228, on [v]D) */
-    fe dl;
-    int ex = fe_is_zero( acc.X );
-    fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
-    int ey = fe_is_zero( dl );
-    code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
-  }
+  int code = verify_tail( args, desc_ok, bad_s, stA, stR, drow, s_dig, tid, gid
+#ifdef FD_PHASE_STAMPS
+                          , _st
+#endif
+                          );
   args.out[ di ] = (int8_t)code;
 #ifdef FD_PHASE_STAMPS
   STAMP( 6 );
@@ -483,6 +518,93 @@ fd_ed25519_verify_kernel( verify_args args ) {
     atomicAdd( &args.stamps[7], 1ull );
   }
 #endif
+}
+
+/* Pair form of the verify kernel, for batches of at most one 256-signature
+   workgroup per CU (config 2's 64K = one wave per SIMD): a 512-thread
+   workgroup gives every signature two lanes in two waves of the same SIMD
+   pair slot -- waves 0-3 (role 0) and waves 4-7 (role 1) hold signatures
+   [256 b, 256 b + 256).  Role 0 does the S check, SHA-512, lattice and
+   digits while role 1 waits at the first barrier; then BOTH run the same
+   decode + table code at once -- role 0 on A, role 1 on R -- so that phase
+   has two waves per SIMD (the single-wave kernel issues one VALU op per ~4.9
+   cycles per SIMD; two waves of the same code fill more of the issue slots;
+   same code, so no extra instruction-cache footprint); role 1 leaves the
+   status of R in LDS and exits after the second barrier, role 0 takes the
+   chain and the tail unchanged.  Bit-identical results to
+   fd_ed25519_verify_kernel (same functions, same order of checks).
+   Measured at 64K: +2.4 % over the single-lane kernel (A/B in one process,
+   FD_ED25519_GPU_PAIR=0).  Waves go to SIMDs round-robin (wave i -> SIMD
+   i mod 4): pairing roles by odd/even wave instead put two chain waves on
+   one SIMD and ran 1.44x slower.  Starting R's decode during role 0's
+   SHA-512 (different code side by side) gained nothing over this order. */
+extern "C" __global__ void __launch_bounds__( 2 * FD_VERIFY_BLOCK, 2 )
+fd_ed25519_verify_pair_kernel( verify_args args ) {
+  __shared__ uint8_t  s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
+  __shared__ uint8_t  s_stR[ FD_VERIFY_BLOCK ];
+
+  int role = (int)threadIdx.x >> 8;                  /* wave-uniform */
+  int tid  = (int)threadIdx.x & (FD_VERIFY_BLOCK - 1);
+  uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)tid;
+  uint64_t cap = args.vtab_cap;
+  uint64_t nn  = args.n;
+  /* no early return before the barriers: waves past n skip the work only */
+  bool wave_live = (gid & ~(uint64_t)63) < nn;
+  bool valid = gid < nn;
+  fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
+  if( valid ) d = args.desc[ gid ];
+  uint64_t asz = args.arena_sz;
+  bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
+                 (uint64_t)d.msg_off + d.msg_sz <= asz;
+  uint32_t lim_dw = (uint32_t)((asz + 3u) >> 2) + 1u;
+
+  uint32_t sig[ 16 ], pub[ 8 ];
+#pragma unroll
+  for( int j=0; j<16; j++ ) sig[j] = 0u;
+#pragma unroll
+  for( int j=0; j<8; j++ ) pub[j] = 0u;
+  if( desc_ok ) {
+    load_words<16>( sig, args.arena, d.sig_off, lim_dw );
+    if( !role ) load_words<8>( pub, args.arena, d.pub_off, lim_dw );
+  }
+  bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                           /* :157-159 */
+  bool live  = desc_ok && !bad_s;
+  uint8_t * drow = s_dig + tid;
+
+  if( !role && wave_live ) {
+    verify_prep_digits( drow, tid, live, sig, pub, args, d, lim_dw
+#ifdef FD_PHASE_STAMPS
+                        , nullptr
+#endif
+                        );
+  }
+  FE_FENCE();
+  __syncthreads();
+
+  /* role 0: A = pub, role 1: R = sig[0:32] -- one decode + table each, at once */
+  int stq = 0;
+  if( live ) {
+    uint32_t enc[ 8 ];
+#pragma unroll
+    for( int j=0; j<8; j++ ) enc[j] = role ? sig[j] : pub[j];
+    ge_p3 Q;
+    int ok = ge_decode( Q, enc, !args.ref_codes );
+    int sm = ge_affine_small_order( Q );
+    FE_FENCE();
+    if( ok && !sm ) vtab_build( args.vtab, cap, (uint64_t)role*cap/2u + gid, Q );
+    stq = (ok ? 1 : 0) | (sm ? 2 : 0);
+    FE_FENCE();
+  }
+  if( role ) s_stR[ tid ] = (uint8_t)stq;
+  __syncthreads();
+  if( role || !valid ) return;
+
+  int code = verify_tail( args, desc_ok, bad_s, stq, (int)s_stR[ tid ], drow, s_dig, tid, gid
+#ifdef FD_PHASE_STAMPS
+                          , nullptr
+#endif
+                          );
+  args.out[ gid ] = (int8_t)code;
 }
 
 /* ------------------------------------------------------------------ SHA-512 batch */

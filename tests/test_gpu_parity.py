@@ -240,3 +240,39 @@ def test_sha512_batch_kats_and_random(gpu):
     got = gpu.sha512_batch(msgs)
     for m, g in zip(msgs, got):
         assert g == hashlib.sha512(m).digest(), (len(m),)
+
+
+def test_pair_and_single_lane_kernels_agree(gpu):
+    """Batches of at most one 256-signature workgroup per CU take the pair
+    kernel (two lanes per signature for the decodes), larger ones the
+    single-lane kernel; FD_ED25519_GPU_PAIR=0 forces the latter.  Both give
+    the golden codes, and a batch one workgroup past the pair limit (single-lane
+    kernel) matches the same records at pair size."""
+    import os
+    recs = _all_golden()
+    arena, desc, sz = fa.pack_batch([(r["msg"], r["sig"], r["pub"]) for r in recs])
+    exp = np.array([r["code"] for r in recs], dtype=np.int8)
+    os.environ["FD_ED25519_GPU_PAIR"] = "0"
+    try:
+        single = fa.Ed25519Gpu(device_mask=1, max_batch=1 << 17)
+    finally:
+        del os.environ["FD_ED25519_GPU_PAIR"]
+    try:
+        assert np.array_equal(single.verify_batch(arena, sz, desc), exp)
+    finally:
+        single.close()
+    assert np.array_equal(gpu.verify_batch(arena, sz, desc), exp)
+    # 256 x CUs signatures (pair kernel) vs 256 x CUs + 256 (single-lane kernel)
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n_pair = 256 * cus
+    recs2, kinds = _corrupted_batch(n_pair + 256, 21)
+    a2, d2, s2 = fa.pack_batch(recs2)
+    g2 = fa.Ed25519Gpu(device_mask=1, max_batch=1 << 17)   # one launch for the whole batch
+    try:
+        big = g2.verify_batch(a2, s2, d2)
+        small = g2.verify_batch(a2, s2, d2[:n_pair])
+    finally:
+        g2.close()
+    assert np.array_equal(big[:n_pair], small)
+    assert np.all(big[kinds == 0] == 0) and np.all(big[kinds == 2] == -1)
