@@ -22,7 +22,17 @@ import statistics
 import sys
 
 
-def pmc(path, kernel="fd_ed25519_verify_kernel"):
+VERIFY_KERNELS = ("fd_ed25519_verify_pair_kernel", "fd_ed25519_verify_kernel")
+
+
+def verify_kernel(path):
+    """The verify kernel the profiled bench launched (config 2 takes the pair kernel)."""
+    names = {r["Kernel_Name"] for r in csv.DictReader(open(path))}
+    return next(k for k in VERIFY_KERNELS if k in names)
+
+
+def pmc(path, kernel=None):
+    kernel = kernel or verify_kernel(path)
     rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"] == kernel]
     by = {}
     for r in rows:
@@ -47,7 +57,8 @@ def main():
     write_kb = statistics.median(d["WRITE_SIZE"] for d in wr)
     hbm = (2.0 * fetch_kb + write_kb) * 1024.0
     traffic = {
-        "batch": n, "kernel": "fd_ed25519_verify_kernel", "launches": len(fe),
+        "batch": n, "kernel": verify_kernel(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv")),
+        "launches": len(fe),
         "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
         "hbm_bytes_per_launch": hbm, "hbm_bytes_per_verify": hbm / n,
         "note": "HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024, medians over the profiled launches of "
@@ -61,13 +72,16 @@ def main():
     waves = sq["SQ_WAVES"]
     out = {k: v for k, v in sq.items()}
     out.update({
+        "kernel": verify_kernel(os.path.join(src, "pmc_sq", "pmc_counter_collection.csv")),
         "valu_instr_per_wave": sq["SQ_INSTS_VALU"] / waves,
+        "valu_instr_per_64_sigs": sq["SQ_INSTS_VALU"] / (n / 64.0),
         "wave_cycles_per_wave": 4.0 * sq["SQ_WAVE_CYCLES"] / waves,
         "wait_any_frac": sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"],
         "cycles_per_valu_instr": 4.0 * sq["SQ_WAVE_CYCLES"] / sq["SQ_INSTS_VALU"],
         "GRBM_GUI_ACTIVE": gr.get("GRBM_GUI_ACTIVE"),
         "effective_clock_ghz": gr.get("GRBM_GUI_ACTIVE", 0) / 8.0 / gr["dur_ns"],
-        "note": "SQ_WAVE_CYCLES / SQ_WAIT_ANY count quad-cycles (x4 = cycles); one wave = 64 signatures",
+        "note": "SQ_WAVE_CYCLES / SQ_WAIT_ANY count quad-cycles (x4 = cycles); the pair kernel runs two waves "
+                "per 64 signatures (one exits after the decodes), the single-lane kernel one",
     })
     json.dump(out, open(os.path.join(dst, "pmc_sq.json"), "w"), indent=1)
 
@@ -77,7 +91,7 @@ def main():
         json.dump({"tool": "tools/issue_probe.hip", "probes": probes}, open(os.path.join(dst, "issue_probe.json"), "w"),
                   indent=1)
     print(json.dumps({"bench": bench["value"], "kernel_ms": bench["roofline"]["kernel_ms"],
-                      "hbm_bytes_per_launch": hbm, "valu_instr_per_wave": out["valu_instr_per_wave"],
+                      "hbm_bytes_per_launch": hbm, "valu_instr_per_64_sigs": out["valu_instr_per_64_sigs"],
                       "cycles_per_valu_instr": out["cycles_per_valu_instr"]}))
 
 
