@@ -268,6 +268,7 @@ __device__ __forceinline__ int wdig( uint8_t const * dig, int k ) {
    16-bit.  Table entries are fetched one step ahead: A's for the next window
    before the doublings, R's before A's addition, the first comb entry during
    the last window. */
+template<bool COMB>
 __device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, uint64_t cap, uint64_t ta, uint64_t tr,
                                           uint8_t const * dig, uint32_t const * ctab, int nw ) {
   ge_identity( acc );
@@ -294,11 +295,12 @@ __device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, ui
     FE_FENCE();
     vtab_finish( q, raw, dbr );
     if( i > 0 ) { dba = dig[ (FD_ROW_U + i-1)*FD_VERIFY_BLOCK ]; vtab_fetch( raw, vtab, cap, ta, dba ); }
-    else        ctab_fetch( craw, ctab, 0, wdig( dig, 0 ) );
+    else if( COMB ) ctab_fetch( craw, ctab, 0, wdig( dig, 0 ) );
     FE_FENCE();
     ge_add_cached( acc, acc, q, i == 0 );
     FE_FENCE();
   }
+  if( !COMB ) return;
 #pragma unroll 1
   for( int k=0; k<FD_CTAB_POS; k++ ) {
     ge_precomp bp;
@@ -306,6 +308,23 @@ __device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, ui
     if( k + 1 < FD_CTAB_POS ) ctab_fetch( craw, ctab, k + 1, wdig( dig, k + 1 ) );
     FE_FENCE();
     ge_madd( acc, acc, bp, k + 1 < FD_CTAB_POS );
+    FE_FENCE();
+  }
+}
+
+/* c = [w]B alone: the 16 comb-table additions of dsm_loop from the identity
+   (the pair kernel's second wave computes it beside the chain). */
+__device__ __forceinline__ void comb_only( ge_p3 & c, uint8_t const * dig, uint32_t const * ctab ) {
+  ge_identity( c );
+  uint32_t craw[ 32 ];
+  ctab_fetch( craw, ctab, 0, wdig( dig, 0 ) );
+#pragma unroll 1
+  for( int k=0; k<FD_CTAB_POS; k++ ) {
+    ge_precomp bp;
+    ctab_finish( bp, craw, wdig( dig, k ) );
+    if( k + 1 < FD_CTAB_POS ) ctab_fetch( craw, ctab, k + 1, wdig( dig, k + 1 ) );
+    FE_FENCE();
+    ge_madd( c, c, bp, true );
     FE_FENCE();
   }
 }
@@ -394,7 +413,8 @@ __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, int tid, boo
    Q = [u](-A) + [v](-R) + [w]B (tables at vtab[gid] / vtab[cap/2 + gid],
    digits in LDS) and Q == O. */
 __device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_ok, bool bad_s, int stA, int stR,
-                                            uint8_t const * drow, uint8_t const * s_dig, int tid, uint64_t gid
+                                            uint8_t const * drow, uint8_t const * s_dig, int tid, uint64_t gid,
+                                            uint32_t const * s_wb  /* NULL: add [w]B here; else its cached form in LDS ([word][256]) */
 #ifdef FD_PHASE_STAMPS
                                             , uint64_t * _st
 #endif
@@ -412,7 +432,19 @@ __device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_
   if( code == 0 ) {
     int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
     ge_p3 acc;
-    dsm_loop( acc, args.vtab, cap, gid, cap/2u + gid, drow, args.ctab, nw );
+    if( !s_wb ) dsm_loop<true>( acc, args.vtab, cap, gid, cap/2u + gid, drow, args.ctab, nw );
+    else {
+      dsm_loop<false>( acc, args.vtab, cap, gid, cap/2u + gid, drow, args.ctab, nw );
+      ge_cached c;
+#pragma unroll
+      for( int j=0; j<10; j++ ) {
+        c.YpX.v[j] = s_wb[ (j     )*FD_VERIFY_BLOCK + tid ]; c.YmX.v[j] = s_wb[ (10 + j)*FD_VERIFY_BLOCK + tid ];
+        c.T2d.v[j] = s_wb[ (20 + j)*FD_VERIFY_BLOCK + tid ]; c.Z2.v[j]  = s_wb[ (30 + j)*FD_VERIFY_BLOCK + tid ];
+      }
+      FE_FENCE();
+      ge_add_cached( acc, acc, c, false );
+      FE_FENCE();
+    }
     STAMP( 5 );
     /* Q == O  <=>  X == 0 and Y == Z (the reference's projective compare, :225-228, on [v]D) */
     fe dl;
@@ -504,7 +536,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
   STAMP( 4 );
 
   if( !valid ) return;
-  int code = verify_tail( args, desc_ok, bad_s, stA, stR, drow, s_dig, tid, gid
+  int code = verify_tail( args, desc_ok, bad_s, stA, stR, drow, s_dig, tid, gid, nullptr
 #ifdef FD_PHASE_STAMPS
                           , _st
 #endif
@@ -530,11 +562,13 @@ fd_ed25519_verify_kernel( verify_args args ) {
    has two waves per SIMD (the single-wave kernel issues one VALU op per ~4.9
    cycles per SIMD; two waves of the same code fill more of the issue slots;
    same code, so no extra instruction-cache footprint); role 1 leaves the
-   status of R in LDS and exits after the second barrier, role 0 takes the
-   chain and the tail unchanged.  Bit-identical results to
+   status of R in LDS, computes [w]B (the 16 comb additions) beside role 0's
+   chain and hands it over in LDS (cached form) at the second barrier; role 0
+   runs the Straus chain and adds it.  Bit-identical results to
    fd_ed25519_verify_kernel (same functions, same order of checks).
-   Measured at 64K: +2.4 % over the single-lane kernel (A/B in one process,
-   FD_ED25519_GPU_PAIR=0).  Waves go to SIMDs round-robin (wave i -> SIMD
+   Measured at 64K, launches of both kernels alternated in one process
+   (tools/ab_kernels.py): 0.672 ms vs 0.683 ms for the single-lane kernel
+   (FD_ED25519_GPU_PAIR=0); the decode pairing alone 0.678.  Waves go to SIMDs round-robin (wave i -> SIMD
    i mod 4): pairing roles by odd/even wave instead put two chain waves on
    one SIMD and ran 1.44x slower.  Starting R's decode during role 0's
    SHA-512 (different code side by side) gained nothing over this order. */
@@ -542,6 +576,7 @@ extern "C" __global__ void __launch_bounds__( 2 * FD_VERIFY_BLOCK, 2 )
 fd_ed25519_verify_pair_kernel( verify_args args ) {
   __shared__ uint8_t  s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
   __shared__ uint8_t  s_stR[ FD_VERIFY_BLOCK ];
+  __shared__ uint32_t s_wb[ FD_VTAB_WORDS * FD_VERIFY_BLOCK ];   /* [w]B, cached form, from role 1 */
 
   int role = (int)threadIdx.x >> 8;                  /* wave-uniform */
   int tid  = (int)threadIdx.x & (FD_VERIFY_BLOCK - 1);
@@ -596,10 +631,23 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
     FE_FENCE();
   }
   if( role ) s_stR[ tid ] = (uint8_t)stq;
+  if( role ) {
+    /* [w]B beside role 0's chain (16 comb additions; w digits came before
+       the first barrier) */
+    ge_p3 c;
+    ge_cached cc;
+    comb_only( c, drow, args.ctab );
+    ge_to_cached( cc, c );
+#pragma unroll
+    for( int j=0; j<10; j++ ) {
+      s_wb[ (j     )*FD_VERIFY_BLOCK + tid ] = cc.YpX.v[j]; s_wb[ (10 + j)*FD_VERIFY_BLOCK + tid ] = cc.YmX.v[j];
+      s_wb[ (20 + j)*FD_VERIFY_BLOCK + tid ] = cc.T2d.v[j]; s_wb[ (30 + j)*FD_VERIFY_BLOCK + tid ] = cc.Z2.v[j];
+    }
+  }
   __syncthreads();
   if( role || !valid ) return;
 
-  int code = verify_tail( args, desc_ok, bad_s, stq, (int)s_stR[ tid ], drow, s_dig, tid, gid
+  int code = verify_tail( args, desc_ok, bad_s, stq, (int)s_stR[ tid ], drow, s_dig, tid, gid, s_wb
 #ifdef FD_PHASE_STAMPS
                           , nullptr
 #endif

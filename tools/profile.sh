@@ -7,7 +7,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-BENCH="bench.py --steps 10 --warmup 2 --no-cpu"
+BENCH="bench.py --no-cpu"
 timeout -k 10 240 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $BENCH > $OUT/kt_bench.json 2> $OUT/kt.err
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2> $OUT/pmc_fetch.err
