@@ -45,7 +45,13 @@ FD_FN void fe_const_sqrtm1( fe & r ) {
 
 FD_FN void ge_identity( ge_p3 & p ) { fe_set0( p.X ); fe_set1( p.Y ); fe_set1( p.Z ); fe_set0( p.T ); }
 
-/* r = 2p (dbl-2008-hwcd, a=-1).  p.X,Y,Z in R.  T computed iff want_t. */
+/* r = 2p (dbl-2008-hwcd, a=-1).  p.X,Y,Z in R.  T computed iff want_t.
+   Operand order of the output products (here and in the additions): E and G
+   are always the first operand, F and H the second, so each premultiplied
+   operand (x2 odd limbs of the first, x19 of the second) is computed once and
+   shared by two products (the compiler merges them): -90 v_mul_lo_u32 and
+   -65 shifts in the pair kernel, 0.674 vs 0.677 ms at 64K
+   (tools/ab_libs.py, profiles/r01/ab_operand_order.txt). */
 FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
   fe XX, YY, ZZ, AA, s, H, G, E, Fn;
   fe_sq( XX, p.X );                     /* R */
@@ -64,7 +70,7 @@ FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
   fe_sub( Fn, s, YY ); fe_carry( Fn, Fn ); /* R  Fn = 2ZZ-G      */
   fe_mul( r.X, E, Fn );
   FE_FENCE();
-  fe_mul( r.Y, H, G );
+  fe_mul( r.Y, G, H );
   FE_FENCE();
   fe_mul( r.Z, G, Fn );
   FE_FENCE();
@@ -91,7 +97,7 @@ FD_GE_FN void ge_add_cached( ge_p3 & r, ge_p3 const & p, ge_cached const & q, bo
   fe_sub( F, D, TT );                   /* M */
   fe_mul( r.X, E, F );
   FE_FENCE();
-  fe_mul( r.Y, H, G );
+  fe_mul( r.Y, G, H );
   FE_FENCE();
   fe_mul( r.Z, G, F );
   FE_FENCE();
@@ -118,7 +124,7 @@ FD_GE_FN void ge_madd( ge_p3 & r, ge_p3 const & p, ge_precomp const & q, bool wa
   fe_sub( F, D, TT ); fe_carry( F, F ); /* R */
   fe_mul( r.X, E, F );
   FE_FENCE();
-  fe_mul( r.Y, H, G );
+  fe_mul( r.Y, G, H );
   FE_FENCE();
   fe_mul( r.Z, G, F );
   FE_FENCE();
