@@ -46,12 +46,15 @@ FD_FN void fe_const_sqrtm1( fe & r ) {
 FD_FN void ge_identity( ge_p3 & p ) { fe_set0( p.X ); fe_set1( p.Y ); fe_set1( p.Z ); fe_set0( p.T ); }
 
 /* r = 2p (dbl-2008-hwcd, a=-1).  p.X,Y,Z in R.  T computed iff want_t.
-   Operand order of the output products (here and in the additions): E and G
-   are always the first operand, F and H the second, so each premultiplied
-   operand (x2 odd limbs of the first, x19 of the second) is computed once and
-   shared by two products (the compiler merges them): -90 v_mul_lo_u32 and
-   -65 shifts in the pair kernel, 0.674 vs 0.677 ms at 64K
-   (tools/ab_libs.py, profiles/r01/ab_operand_order.txt). */
+   Operand order of the output products (here and in the additions): each
+   premultiplied operand (x2 odd limbs of the first, x19 of the second) is
+   computed once and shared by two products (the compiler merges them; the
+   E/G-first order of the first change: -90 v_mul_lo_u32 and -65 shifts in
+   the pair kernel, 0.674 vs 0.677 ms at 64K, profiles/r01/ab_operand_order.txt).
+   Here and in ge_madd, F and H are the FIRST operands and E, G the second:
+   F is then left uncarried (bound class "F" of fd_f25519_dev.h: its x19 would
+   not fit 32 bits, its x2 does, and F x M column sums stay below 2^63),
+   which drops one fe_carry per doubling / mixed addition. */
 FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
   fe XX, YY, ZZ, AA, s, H, G, E, Fn;
   fe_sq( XX, p.X );                     /* R */
@@ -67,14 +70,14 @@ FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
   fe_sub( G, YY, XX );                  /* M   G = YY-XX          */
   fe_sub( E, AA, H );                   /* M   E = (X+Y)^2-YY-XX = 2XY */
   fe_add( s, ZZ, ZZ ); fe_add( s, s, XX );
-  fe_sub( Fn, s, YY ); fe_carry( Fn, Fn ); /* R  Fn = 2ZZ-G      */
-  fe_mul( r.X, E, Fn );
+  fe_sub( Fn, s, YY );                  /* F   Fn = 2ZZ-G, not carried: first operand only */
+  fe_mul( r.X, Fn, E );
   FE_FENCE();
-  fe_mul( r.Y, G, H );
+  fe_mul( r.Y, H, G );
   FE_FENCE();
-  fe_mul( r.Z, G, Fn );
+  fe_mul( r.Z, Fn, G );
   FE_FENCE();
-  if( want_t ) fe_mul( r.T, E, H );
+  if( want_t ) fe_mul( r.T, H, E );
   FE_FENCE();
 }
 
@@ -121,14 +124,14 @@ FD_GE_FN void ge_madd( ge_p3 & r, ge_p3 const & p, ge_precomp const & q, bool wa
   fe_sub( E, PP, MM );                  /* M */
   fe_add( H, PP, MM );                  /* M */
   fe_add( G, D, TT );                   /* 3R -> M */
-  fe_sub( F, D, TT ); fe_carry( F, F ); /* R */
-  fe_mul( r.X, E, F );
+  fe_sub( F, D, TT );                   /* F (4R + ...), not carried: first operand only */
+  fe_mul( r.X, F, E );
   FE_FENCE();
-  fe_mul( r.Y, G, H );
+  fe_mul( r.Y, H, G );
   FE_FENCE();
-  fe_mul( r.Z, G, F );
+  fe_mul( r.Z, F, G );
   FE_FENCE();
-  if( want_t ) fe_mul( r.T, E, H );
+  if( want_t ) fe_mul( r.T, H, E );
   FE_FENCE();
 }
 

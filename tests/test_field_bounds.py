@@ -17,6 +17,7 @@ LL = 2**252 + 27742317777372353535851937790883648493
 POS = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
 R_E, R_O = 2**26 + 2**11, 2**25 + 2**16
 M_E, M_O = 3 * 2**26 + 2**13, 3 * 2**25 + 2**18
+F_E, F_O = 5 * 2**26 + 3 * 2**11, 5 * 2**25 + 3 * 2**16   # "F": uncarried first operand (fd_f25519_dev.h)
 
 
 @pytest.fixture(scope="module")
@@ -55,6 +56,25 @@ def test_mul_sq_at_bounds(lib):
         assert val(h) % P == val(f) * val(g) % P and in_R(h)
         h = (ctypes.c_uint32 * 10)(); lib.t_sq(h, arr(f)); h = list(h)
         assert val(h) % P == val(f) ** 2 % P and in_R(h)
+
+
+def test_mul_uncarried_first_operand(lib):
+    """fe_mul( h, F, M ): the doubling's Fn = 2ZZ + XX + 2p - YY and the mixed
+    addition's F = 2Z + 2p - TT go in uncarried as the first operand
+    (fd_curve25519_dev.h ge_dbl / ge_madd); the product stays exact and in R."""
+    rng = random.Random(7)
+    for it in range(3000):
+        mode = "max" if it < 20 else "rand"
+        f = limbs_at(F_E, F_O, mode, rng); g = limbs_at(M_E, M_O, mode, rng)
+        h = (ctypes.c_uint32 * 10)(); lib.t_mul(h, arr(f), arr(g)); h = list(h)
+        assert val(h) % P == val(f) * val(g) % P and in_R(h)
+    # the operands as the formulas build them, at their own maxima
+    r = [R_E if i % 2 == 0 else R_O for i in range(10)]
+    two_p = [2 * (2**26 - 19)] + [2 * (2**26 - 1) if i % 2 == 0 else 2 * (2**25 - 1) for i in range(1, 10)]
+    fn = [3 * r[i] + two_p[i] for i in range(10)]            # 2ZZ + XX + 2p - 0
+    assert all(x <= (F_E if i % 2 == 0 else F_O) for i, x in enumerate(fn))
+    fm = [2 * r[i] + two_p[i] for i in range(10)]            # 2Z + 2p - 0
+    assert all(x <= (F_E if i % 2 == 0 else F_O) for i, x in enumerate(fm))
 
 
 def test_sub_carry_canon(lib):
