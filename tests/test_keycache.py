@@ -106,3 +106,31 @@ def test_fresh_signatures_hot_keys(kgpu):
     bad = np.nonzero(out != exp)[0]
     assert len(bad) == 0, [(int(i), int(out[i]), int(exp[i])) for i in bad[:10]]
     assert (exp == 0).sum() > n // 5
+
+
+@pytest.mark.gpu
+def test_all_cached_device_entry_bench_shape():
+    """The bench's --hot-keys shape through the device-pointer entry: every
+    signer cached, so the miss list is empty and only the split and the
+    cached kernel do work (a launch whose split-kernel arguments carried a
+    stale device-count pointer faulted here; the host now zeroes them)."""
+    import torch
+    sys.path.insert(0, REPO)
+    import bench
+    n = 16384
+    arena, desc, sz, expect, _ = bench.build_workload(n, 200, seed=3, n_keys=256)
+    g = fa.Ed25519Gpu(device_mask=1, max_batch=n)
+    try:
+        keys = sorted(set(bench.desc_pub(arena, desc)))
+        g.keycache_reserve(len(keys))
+        assert g.keycache_add(keys) == len(keys) == 256
+        d_arena = torch.from_numpy(arena).cuda()
+        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
+        d_out = torch.full((n,), 99, dtype=torch.int8, device="cuda")
+        st = torch.cuda.Stream()
+        for _ in range(3):
+            g.verify_batch_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, d_out.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_out.cpu().numpy(), expect)
+    finally:
+        g.close()
