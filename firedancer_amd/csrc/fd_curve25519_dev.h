@@ -26,7 +26,7 @@
 #endif
 
 struct ge_p3     { fe X, Y, Z, T; };          /* all R */
-struct ge_cached { fe YpX, YmX, T2d, Z2; };   /* (Y+X, Y-X, 2dT, 2Z), all R */
+struct ge_cached { fe YpX, YmX, T2d, Z2; };   /* (Y+X, Y-X, 2dT, 2Z): 2dT in R, the others in M */
 struct ge_precomp{ fe YpX, YmX, T2d; };       /* affine (Z=1) form of ge_cached */
 
 /* d, 2d, sqrt(-1) in radix 2^25.5 (derived: d = -121665/121666 mod p) */
@@ -135,13 +135,16 @@ FD_GE_FN void ge_madd( ge_p3 & r, ge_p3 const & p, ge_precomp const & q, bool wa
   FE_FENCE();
 }
 
+/* Cached form.  Y+X, Y-X and 2Z are left uncarried (M): every consumer
+   (ge_add_cached, through vtab_finish's swap) uses them only as the second
+   operand of fe_mul, which takes M.  T2d stays R (vtab_finish negates it). */
 FD_FN void ge_to_cached( ge_cached & c, ge_p3 const & p ) {
   fe d2; fe_const_d2( d2 );
-  fe_add_r( c.YpX, p.Y, p.X );
-  fe_sub_r( c.YmX, p.Y, p.X );
+  fe_add( c.YpX, p.Y, p.X );
+  fe_sub( c.YmX, p.Y, p.X );
   fe_mul( c.T2d, p.T, d2 );
   FE_FENCE();
-  fe_add_r( c.Z2, p.Z, p.Z );
+  fe_add( c.Z2, p.Z, p.Z );
 }
 
 /* 1/z = z^(p-2) = (z^(2^252-3))^8 * z^3 */
