@@ -4,10 +4,18 @@
 Workload (BASELINE.json configs[1], "config 2"): per GPU, a 65,536-signature
 batch with fixed 200-byte messages, all valid (the most work per signature),
 inputs resident in HBM before the timed region.  One step = one pass of the
-verify hot path (fd_ed25519_verify_batch_gpu_dev) over that batch.  With
---gpus N (torch.distributed.run, one process per GPU) every rank verifies its
-own 64K batch: weak scaling, no collective on the data path (signatures are
-independent; the barrier + MAX-over-ranks timing is the only exchange).
+verify hot path (fd_ed25519_verify_batch_gpu_dev) over that batch.
+
+Multi-GPU: `--gpus N` runs N ranks, one process per GPU.  Started without
+WORLD_SIZE (plain `python bench.py --gpus N`), bench.py checks that N devices
+are visible (exit 2 otherwise, before anything touches a GPU) and runs itself
+under torch.distributed.run as a child process; started by
+torch.distributed.run (the driver's form), WORLD_SIZE must equal N.  Every
+rank verifies its own 64K batch: weak scaling, no collective on the data path
+(signatures are independent, the reference scales the same way with N
+independent verify tiles, src/app/fdctl/run/tiles/fd_verify.c:140-141); the
+barrier + SUM(units) / MAX(time) over ranks is the only exchange.
+`--stub` runs the same launcher and aggregation on CPU (gloo) for the tests.
 
 Synthetic data: 65,536 distinct keys and 200-byte random messages per rank
 (fixed seed), RFC 8032-signed on the host by the benchmark input generator
@@ -113,31 +121,64 @@ def pmc_traffic(n):
 
 
 def cpu_baseline(arena, desc, expect, budget_s=10.0):
-    """Reference fd_ed25519_verify on this host, bounded sample (oracle/_ref)."""
+    """Reference fd_ed25519_verify on this host (oracle/_ref), bounded sample:
+    one pinned thread per physical core this process may use (BASELINE.md /
+    SURVEY.md §8(d): N = physical cores, N stated), each verifying a
+    contiguous shard of the same descriptors, warm-up pass, then whole passes
+    until the budget is spent."""
+    from firedancer_amd.hostcpu import baseline_cpus
     has_ifma = "avx512ifma" in open("/proc/cpuinfo").read()
     flavour = "avx512" if has_ifma else "ref"
     path = os.path.join(REPO, "oracle", "_ref", "libfdref_%s.so" % flavour)
-    threads = min(16, os.cpu_count() or 1)
     if not os.path.exists(path):
         return None
+    cpus, topo = baseline_cpus()
+    threads = min(len(cpus), 256)
+    cpu_arr = (ctypes.c_int * threads)(*cpus[:threads])
     lib = ctypes.CDLL(path)
-    lib.fdref_verify_descs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
-                                       ctypes.c_ulong, ctypes.c_ulong]
-    m = min(len(desc), 16384)
+    lib.fdref_verify_descs_pinned.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                                              ctypes.c_ulong, ctypes.c_ulong, ctypes.c_void_p]
+    m = min(len(desc), 65536)
     d = np.ascontiguousarray(desc[:m])
     out = np.zeros(m, np.int8)
     vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-    lib.fdref_verify_descs(vp(arena), vp(d), m, vp(out), threads, 1)   # warm-up pass
+    lib.fdref_verify_descs_pinned(vp(arena), vp(d), m, vp(out), threads, 1, cpu_arr)   # warm-up pass
     if flavour == "avx512":
         assert np.array_equal(out, expect[:m]), "reference codes differ from the expected ones"
     t0 = time.perf_counter(); done = 0
     while time.perf_counter() - t0 < budget_s:
-        lib.fdref_verify_descs(vp(arena), vp(d), m, vp(out), threads, 1)
+        lib.fdref_verify_descs_pinned(vp(arena), vp(d), m, vp(out), threads, 1, cpu_arr)
         done += m
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "verifies/s", "cores": threads, "kind": "reference",
+    value = done / dt
+    return {"value": value, "unit": "verifies/s", "cores": threads, "kind": "reference",
+            "per_core": value / threads, "topology": topo,
             "sample": "%d passes x %d of the same descriptors (%.1f s), fd_ed25519_verify %s build, "
-                      "%d pthreads" % (done // m, m, dt, "FD_HAS_AVX512" if has_ifma else "ref", threads)}
+                      "%d pthreads pinned one per physical core" % (done // m, m, dt,
+                                                                    "FD_HAS_AVX512" if has_ifma else "ref", threads)}
+
+
+def launch_ranks(args):
+    """--gpus N without WORLD_SIZE: run N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process and return its exit code.  The
+    device count is read before anything initialises the GPU in this process
+    (torch.cuda.device_count() does not, on this image); fewer devices than N
+    is an error, never a silent single-GPU run."""
+    import socket
+    import subprocess
+    if not args.stub:
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print("bench.py: --gpus %d but only %d GPU(s) visible; refusing to run" % (args.gpus, have),
+                  file=sys.stderr, flush=True)
+            return 2
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -158,26 +199,42 @@ def main():
     ap.add_argument("--msg-sz", type=int, default=200)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prime-ms", type=float, default=150.0,
+                    help="untimed back-to-back steps for this long before the warm-up steps: a GPU that was idle "
+                         "runs its first ~100 ms at a ramping clock; the timed region should see the clock a "
+                         "continuously fed verify stage runs at (reported as prime_steps)")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU test mode (tests/test_bench_launch.py): gloo, a no-op step on a fixed count; "
+                         "exercises the launcher, rank setup and SUM/MAX aggregation without a GPU")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.stub:
+        sys.exit(stub_main(args, world, rank))
 
     import torch
     import torch.distributed as dist
     import firedancer_amd as fa
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.device_count() <= local:
+        print("bench.py: rank %d needs GPU %d, %d visible" % (rank, local, torch.cuda.device_count()),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend="nccl", device_id=dev)
 
     def barrier():
         if world > 1:
-            if dist.get_backend() == "nccl":
-                dist.barrier(device_ids=[local])
-            else:
-                dist.barrier()
+            dist.barrier(device_ids=[local])
 
     if args.config == 3:
         total = args.batch or 1 << 20
@@ -207,6 +264,13 @@ def main():
         g.verify_batch_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, d_out.data_ptr(),
                            stream=stream.cuda_stream)
 
+    prime = 0
+    t_prime = time.perf_counter()
+    while (time.perf_counter() - t_prime) * 1e3 < args.prime_ms:
+        for _ in range(8):
+            step()
+        prime += 8
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -257,6 +321,7 @@ def main():
                          "frac": achieved / peak, "traffic": pmc_traffic(n) if args.config == 2 and not args.hot_keys else None,
                          "kernel_ms": launch_ms},
             "cpu_baseline": None,
+            "prime_steps": prime,
         }
         # The same launch against the HBM roofline (not the bound: ~1/6 of the ~8 TB/s peak),
         # from the PMC-measured bytes per launch of profiles/r01/pmc_traffic.json.
@@ -273,6 +338,36 @@ def main():
     g.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def stub_main(args, world, rank):
+    """--stub: the launcher / aggregation path on CPU (gloo), no GPU, no HIP.
+    Each rank 'verifies' a fixed count per step (a short sleep stands in for
+    the kernel); the line reports SUM of units over ranks / MAX of time."""
+    import torch.distributed as dist
+    from firedancer_amd.dist import aggregate_throughput
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    n = args.batch or 1024
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.002 * (1 + rank))
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    total, dt_max = aggregate_throughput(n * args.steps, dt)
+    if rank == 0:
+        print(json.dumps({"metric": "Ed25519 verifies/sec", "value": total / dt_max, "unit": "verifies/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "stub": True, "units_total": total, "seconds_max": dt_max}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

@@ -1,5 +1,15 @@
 /* fd_verify_offload.cpp -- the shared-memory link of include/fd_verify_offload.h
-   (client + server primitives; no HIP, so a sandboxed tile can link it). */
+   (client + server primitives; no HIP, so a sandboxed tile can link it).
+
+   Trust: the two sides share the header, and either may be faulty or
+   hostile (the client is a sandboxed tile).  The ring geometry (depth,
+   frag-area size, region offsets) is therefore read from the header ONCE,
+   validated (create writes it, join checks that every region lies inside the
+   mapping and depth is a power of two), and kept in each side's private
+   handle; every index afterwards uses the private copy.  The server's
+   consumer cursor lives in its private handle and is only published to the
+   header (one way).  Frag records the client wrote are bounds-checked by
+   the consumer (fd_verify_offload_serve snapshots them first). */
 
 #include "../../include/fd_verify_offload.h"
 
@@ -32,19 +42,47 @@ struct fd_verify_offload {
   int8_t *   res;
   uint64_t * sig;
   uint8_t *  dcache;
+  /* private copies of the validated geometry (never re-read from h) */
+  uint64_t   depth, mask, dcache_sz;
+  /* server (creator): its consumer cursor, published to h->cons_seq */
+  uint64_t   cons;
+  int        server;
 };
 
 static uint64_t align_up( uint64_t x, uint64_t a ) { return (x + a - 1u) & ~(a - 1u); }
 
+/* [off, off + n*sz) inside [lo, footprint), without overflow */
+static int region_ok( uint64_t off, uint64_t n, uint64_t sz, uint64_t lo, uint64_t footprint ) {
+  if( off < lo || off > footprint ) return 0;
+  if( sz && n > (footprint - off) / sz ) return 0;
+  return 1;
+}
+
+/* Geometry check of a header snapshot against the mapping size. */
+static int geometry_ok( hdr const * g, uint64_t footprint ) {
+  uint64_t depth = g->depth, dsz = g->dcache_sz;
+  if( !depth || (depth & (depth - 1u)) || depth > (1ull << 32) ) return 0;
+  if( !dsz || (dsz & (LINE - 1u)) || dsz > 0xffffffffull ) return 0;
+  if( (g->frag_off & 7u) || (g->sig_off & 7u) ) return 0;
+  uint64_t lo = sizeof(hdr);
+  return region_ok( g->frag_off, depth, sizeof(fd_verify_offload_frag_t), lo, footprint ) &&
+         region_ok( g->res_off, depth, 1u, lo, footprint ) &&
+         region_ok( g->sig_off, depth, sizeof(uint64_t), lo, footprint ) &&
+         region_ok( g->dcache_off, dsz, 1u, lo, footprint );
+}
+
 static fd_verify_offload_t *
-wrap( uint8_t * base, uint64_t footprint ) {
+wrap( uint8_t * base, uint64_t footprint, hdr const * g, int server ) {
   fd_verify_offload_t * o = (fd_verify_offload_t *)calloc( 1, sizeof(*o) );
   if( !o ) return NULL;
   o->base = base; o->footprint = footprint; o->h = (hdr *)base;
-  o->frag   = (fd_verify_offload_frag_t *)(base + o->h->frag_off);
-  o->res    = (int8_t *)(base + o->h->res_off);
-  o->sig    = (uint64_t *)(base + o->h->sig_off);
-  o->dcache = base + o->h->dcache_off;
+  o->frag   = (fd_verify_offload_frag_t *)(base + g->frag_off);
+  o->res    = (int8_t *)(base + g->res_off);
+  o->sig    = (uint64_t *)(base + g->sig_off);
+  o->dcache = base + g->dcache_off;
+  o->depth = g->depth; o->mask = g->depth - 1u; o->dcache_sz = g->dcache_sz;
+  o->server = server;
+  o->cons = 0u;
   return o;
 }
 
@@ -67,8 +105,9 @@ fd_verify_offload_create( char const * name, uint64_t depth, uint64_t dcache_sz 
   hdr * h = (hdr *)p;
   h->depth = depth; h->dcache_sz = dcache_sz; h->footprint = footprint;
   h->frag_off = frag_off; h->res_off = res_off; h->sig_off = sig_off; h->dcache_off = dcache_off;
+  hdr g = *h;                                                  /* the server's own geometry, not re-read */
   __atomic_store_n( &h->magic, FD_VERIFY_OFFLOAD_MAGIC, __ATOMIC_RELEASE );
-  fd_verify_offload_t * o = wrap( (uint8_t *)p, footprint );
+  fd_verify_offload_t * o = wrap( (uint8_t *)p, footprint, &g, 1 );
   if( !o ) { munmap( p, footprint ); shm_unlink( name ); }
   return o;
 }
@@ -85,10 +124,11 @@ fd_verify_offload_join( char const * name ) {
   close( fd );
   if( p == MAP_FAILED ) return NULL;
   hdr * h = (hdr *)p;
-  if( __atomic_load_n( &h->magic, __ATOMIC_ACQUIRE ) != FD_VERIFY_OFFLOAD_MAGIC || h->footprint != footprint ) {
-    munmap( p, footprint ); return NULL;
-  }
-  fd_verify_offload_t * o = wrap( (uint8_t *)p, footprint );
+  if( __atomic_load_n( &h->magic, __ATOMIC_ACQUIRE ) != FD_VERIFY_OFFLOAD_MAGIC ) { munmap( p, footprint ); return NULL; }
+  hdr g;
+  memcpy( &g, h, sizeof(g) );                                  /* one snapshot: checked and used */
+  if( g.footprint != footprint || !geometry_ok( &g, footprint ) ) { munmap( p, footprint ); return NULL; }
+  fd_verify_offload_t * o = wrap( (uint8_t *)p, footprint, &g, 0 );
   if( !o ) munmap( p, footprint );
   return o;
 }
@@ -102,8 +142,8 @@ fd_verify_offload_leave( fd_verify_offload_t * o ) {
 
 extern "C" int fd_verify_offload_unlink( char const * name ) { return name ? shm_unlink( name ) : -1; }
 
-extern "C" uint64_t fd_verify_offload_depth    ( fd_verify_offload_t const * o ) { return o->h->depth;     }
-extern "C" uint64_t fd_verify_offload_dcache_sz( fd_verify_offload_t const * o ) { return o->h->dcache_sz; }
+extern "C" uint64_t fd_verify_offload_depth    ( fd_verify_offload_t const * o ) { return o->depth;     }
+extern "C" uint64_t fd_verify_offload_dcache_sz( fd_verify_offload_t const * o ) { return o->dcache_sz; }
 
 /* ---- client ---- */
 
@@ -111,16 +151,19 @@ extern "C" int64_t
 fd_verify_offload_publish( fd_verify_offload_t * o, uint8_t const * frag, uint32_t sz ) {
   if( !o || !frag || !sz ) return FD_VERIFY_OFFLOAD_ERR_ARG;
   hdr * h = o->h;
-  uint64_t need = align_up( sz, LINE ), cap = h->dcache_sz;
+  uint64_t need = align_up( sz, LINE ), cap = o->dcache_sz;
   if( need > cap ) return FD_VERIFY_OFFLOAD_ERR_ARG;
   uint64_t prod = h->prod_seq;                                           /* own line */
   uint64_t done = __atomic_load_n( &h->done_seq, __ATOMIC_ACQUIRE );
-  if( prod - done >= h->depth ) return FD_VERIFY_OFFLOAD_ERR_FULL;
+  if( done > prod ) return FD_VERIFY_OFFLOAD_ERR_SEQ;                    /* a server past our frags: corrupt */
+  if( prod - done >= o->depth ) return FD_VERIFY_OFFLOAD_ERR_FULL;
   /* In-flight bytes are [oldest, cursor) cyclically (frags are placed FIFO). */
   uint64_t cur = h->cursor, at;
+  if( cur > cap ) cur = cap;
   if( prod == done ) at = 0u;                 /* nothing in flight: restart at the front */
   else {
-    uint64_t oldest = o->frag[ done & (h->depth - 1u) ].off;
+    uint64_t oldest = o->frag[ done & o->mask ].off;
+    if( oldest > cap ) return FD_VERIFY_OFFLOAD_ERR_SEQ;
     if( cur > oldest ) {                        /* used: [oldest, cur) */
       if( cur + need <= cap ) at = cur;
       else if( need <= oldest ) at = 0u;
@@ -131,7 +174,7 @@ fd_verify_offload_publish( fd_verify_offload_t * o, uint8_t const * frag, uint32
     }
   }
   memcpy( o->dcache + at, frag, sz );
-  fd_verify_offload_frag_t * r = &o->frag[ prod & (h->depth - 1u) ];
+  fd_verify_offload_frag_t * r = &o->frag[ prod & o->mask ];
   r->off = (uint32_t)at; r->sz = sz;
   h->cursor = at + need;
   __atomic_store_n( &h->prod_seq, prod + 1u, __ATOMIC_RELEASE );
@@ -143,10 +186,10 @@ fd_verify_offload_result( fd_verify_offload_t const * o, uint64_t seq, int8_t * 
   if( !o ) return FD_VERIFY_OFFLOAD_ERR_ARG;
   hdr const * h = o->h;
   uint64_t prod = __atomic_load_n( &h->prod_seq, __ATOMIC_ACQUIRE );
-  if( seq >= prod || prod - seq > h->depth ) return FD_VERIFY_OFFLOAD_ERR_SEQ;
+  if( seq >= prod || prod - seq > o->depth ) return FD_VERIFY_OFFLOAD_ERR_SEQ;
   uint64_t done = __atomic_load_n( &h->done_seq, __ATOMIC_ACQUIRE );
   if( seq >= done ) return 0;
-  uint64_t i = seq & (h->depth - 1u);
+  uint64_t i = seq & o->mask;
   if( result ) *result = o->res[ i ];
   if( sig )    *sig    = o->sig[ i ];
   return 1;
@@ -165,8 +208,9 @@ fd_verify_offload_results( fd_verify_offload_t const * o, uint64_t seq, uint64_t
   hdr const * h = o->h;
   uint64_t prod = __atomic_load_n( &h->prod_seq, __ATOMIC_ACQUIRE );
   uint64_t done = __atomic_load_n( &h->done_seq, __ATOMIC_ACQUIRE );
-  if( seq >= done || prod - seq > h->depth ) return 0u;
-  uint64_t m = done - seq < n ? done - seq : n, mask = h->depth - 1u;
+  if( seq >= done || prod - seq > o->depth ) return 0u;
+  uint64_t m = done - seq < n ? done - seq : n, mask = o->mask;
+  if( m > o->depth ) m = o->depth;
   for( uint64_t i=0; i<m; i++ ) {
     if( result ) result[ i ] = o->res[ (seq + i) & mask ];
     if( sig )    sig[ i ]    = o->sig[ (seq + i) & mask ];
@@ -181,26 +225,35 @@ extern "C" void     fd_verify_offload_halt    ( fd_verify_offload_t * o )       
 /* ---- server primitives ---- */
 
 extern "C" int      fd_verify_offload_halted  ( fd_verify_offload_t const * o ) { return (int)__atomic_load_n( &o->h->halt, __ATOMIC_ACQUIRE ); }
-extern "C" uint64_t fd_verify_offload_cons_seq( fd_verify_offload_t const * o ) { return o->h->cons_seq; }
+/* The consumer cursor: the server's private copy (the header's cons_seq is
+   only an outbound report); a non-server handle reads the report. */
+extern "C" uint64_t fd_verify_offload_cons_seq( fd_verify_offload_t const * o ) {
+  return o->server ? o->cons : __atomic_load_n( &o->h->cons_seq, __ATOMIC_ACQUIRE );
+}
 
 extern "C" uint64_t
 fd_verify_offload_avail( fd_verify_offload_t const * o, uint64_t * first_seq ) {
   hdr const * h = o->h;
   uint64_t prod = __atomic_load_n( &h->prod_seq, __ATOMIC_ACQUIRE );
-  uint64_t cons = h->cons_seq;
+  uint64_t cons = fd_verify_offload_cons_seq( o );
   if( first_seq ) *first_seq = cons;
+  if( prod <= cons ) return 0u;                                 /* nothing new (or a client gone backwards) */
   uint64_t n = prod - cons;
-  uint64_t to_end = h->depth - (cons & (h->depth - 1u));
+  if( n > o->depth ) n = o->depth;                              /* a client cannot have more than depth in flight */
+  uint64_t to_end = o->depth - (cons & o->mask);
   return n < to_end ? n : to_end;
 }
 
 extern "C" fd_verify_offload_frag_t const *
-fd_verify_offload_frag_laddr( fd_verify_offload_t const * o, uint64_t seq ) { return &o->frag[ seq & (o->h->depth - 1u) ]; }
-extern "C" int8_t *   fd_verify_offload_result_laddr( fd_verify_offload_t * o, uint64_t seq ) { return &o->res[ seq & (o->h->depth - 1u) ]; }
-extern "C" uint64_t * fd_verify_offload_sig_laddr   ( fd_verify_offload_t * o, uint64_t seq ) { return &o->sig[ seq & (o->h->depth - 1u) ]; }
+fd_verify_offload_frag_laddr( fd_verify_offload_t const * o, uint64_t seq ) { return &o->frag[ seq & o->mask ]; }
+extern "C" int8_t *   fd_verify_offload_result_laddr( fd_verify_offload_t * o, uint64_t seq ) { return &o->res[ seq & o->mask ]; }
+extern "C" uint64_t * fd_verify_offload_sig_laddr   ( fd_verify_offload_t * o, uint64_t seq ) { return &o->sig[ seq & o->mask ]; }
 extern "C" uint8_t *  fd_verify_offload_dcache      ( fd_verify_offload_t * o ) { return o->dcache; }
 
-extern "C" void fd_verify_offload_take    ( fd_verify_offload_t * o, uint64_t cnt ) { o->h->cons_seq += cnt; }
+extern "C" void fd_verify_offload_take( fd_verify_offload_t * o, uint64_t cnt ) {
+  o->cons += cnt;
+  __atomic_store_n( &o->h->cons_seq, o->cons, __ATOMIC_RELEASE );
+}
 extern "C" void fd_verify_offload_complete( fd_verify_offload_t * o, uint64_t done_seq ) {
   __atomic_store_n( &o->h->done_seq, done_seq, __ATOMIC_RELEASE );
 }

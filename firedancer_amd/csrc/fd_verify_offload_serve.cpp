@@ -16,6 +16,8 @@
 #include "../../include/fd_verify_offload.h"
 
 #include <time.h>
+#include <string.h>
+#include <vector>
 
 static inline uint64_t now_ns( void ) {
   struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
@@ -37,16 +39,24 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
   int err = FD_ED25519_GPU_OK;
   uint8_t * dc = fd_verify_offload_dcache( off );
   uint64_t dsz = fd_verify_offload_dcache_sz( off );
+  /* Private snapshots of the frag records of the (up to two) batches in
+     flight: the client can rewrite the shared ring at any time, so the stage
+     parses (and bounds-checks against dsz) a copy it alone owns. */
+  std::vector<fd_ed25519_gpu_frag_t> snap[ 2 ];
+  snap[ 0 ].resize( max_batch ); snap[ 1 ].resize( max_batch );
+  int snap_next = 0;
   for(;;) {
     int progressed = 0;
     uint64_t first, avail = fd_verify_offload_avail( off, &first );
     if( q < 2 && avail && (q == 0 || avail >= max_batch/2u) ) {
       uint64_t m = avail < max_batch ? avail : max_batch;
-      fd_verify_offload_frag_t const * f = fd_verify_offload_frag_laddr( off, first );
+      fd_ed25519_gpu_frag_t * f = snap[ snap_next ].data();
+      memcpy( f, fd_verify_offload_frag_laddr( off, first ), m * sizeof(fd_ed25519_gpu_frag_t) );
+      snap_next ^= 1;
       for( uint64_t j=1; j<m; j++ ) if( f[ j ].off < f[ j-1 ].off ) { m = j; break; }   /* frag-area wrap */
       uint64_t t0 = now_ns();
       if( !t_first ) t_first = t0;
-      err = fd_ed25519_gpu_stage_submit( st, dc, dsz, (fd_ed25519_gpu_frag_t const *)f, m,
+      err = fd_ed25519_gpu_stage_submit( st, dc, dsz, f, m,
                                          fd_verify_offload_result_laddr( off, first ),
                                          fd_verify_offload_sig_laddr( off, first ) );
       if( err ) break;

@@ -73,6 +73,12 @@ typedef struct fd_ed25519_gpu fd_ed25519_gpu_t;
    descriptors per call (device buffers are sized for it; larger calls are
    split internally).  Returns NULL on failure (no device / OOM). */
 fd_ed25519_gpu_t * fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch );
+/* Same over an explicit list of shard slots: slot j runs on HIP device
+   dev_ids[j] with its own stream, tables and scratch; a device may appear
+   more than once (two slots on one GPU run their shards of a batch as two
+   concurrent streams, and let the multi-device sharding be tested on one
+   GPU).  fd_ed25519_gpu_new( mask ) == new_devs( the set bits of mask ). */
+fd_ed25519_gpu_t * fd_ed25519_gpu_new_devs( int const * dev_ids, int ndev, uint64_t max_batch );
 void               fd_ed25519_gpu_delete( fd_ed25519_gpu_t * ctx );
 int                fd_ed25519_gpu_device_cnt( fd_ed25519_gpu_t const * ctx );
 
@@ -105,7 +111,10 @@ int fd_ed25519_gpu_host_unregister( fd_ed25519_gpu_t * ctx, void * p );
    unchanged (bit-exact either way).  reserve sizes the cache (per device:
    capacity x 512 KB + lists for max_batch signatures; clears it); add
    inserts keys (32 B each; already-cached keys are skipped; stops when
-   full) and returns how many were added. */
+   full) and returns how many were added.  add builds every device's tables
+   before it publishes the new keys (on failure none of them is cached);
+   reserve / add / clear wait for launches that may read the cache and
+   return FD_ED25519_GPU_ERR_BUSY while a submit or frag batch is pending. */
 int      fd_ed25519_gpu_keycache_reserve( fd_ed25519_gpu_t * ctx, uint64_t capacity );
 int64_t  fd_ed25519_gpu_keycache_add    ( fd_ed25519_gpu_t * ctx, uint8_t const * pubkeys, uint64_t n );
 uint64_t fd_ed25519_gpu_keycache_cnt    ( fd_ed25519_gpu_t const * ctx );
@@ -121,9 +130,13 @@ int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64
 int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * ctx );
 
 /* Device-resident entry point (no host copies): d_arena / d_desc / d_out are
-   device pointers on the context's device dev_idx, stream is a hipStream_t
-   (NULL = the context's own stream for that device).  d_arena must be
-   readable up to align_up(arena_sz, 4) + 8 bytes.  Enqueues and returns. */
+   device pointers on the context's shard slot dev_idx, stream is a
+   hipStream_t (NULL = the context's own stream for that slot).  d_arena must
+   be readable up to align_up(arena_sz, 4) + 8 bytes.  Enqueues and returns.
+   The slot's table scratch is shared by every launch on it: each launch, on
+   any stream, is ordered after the previous one (an event on the slot), so
+   batches on different streams -- and alongside submit or the verify stage
+   -- never overwrite each other's tables; they run one after another. */
 int fd_ed25519_verify_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx,
                                      uint8_t const * d_arena, uint64_t arena_sz,
                                      fd_ed25519_desc_t const * d_desc, uint64_t desc_cnt,
@@ -143,9 +156,10 @@ int fd_ed25519_gpu_verify_batch_single_msg( fd_ed25519_gpu_t * ctx, uint8_t cons
    (fd_ed25519_user.c:231-309): the first (lowest index) ERR_SIG/ERR_PUBKEY
    of a txn wins, else ERR_MSG if any signature failed the equation, else
    SUCCESS.  A txn's signatures are the maximal runs of equal txn_idx.
-   out_txn_code[t] is written for the t-th run; returns the run count, or
-   FD_ED25519_GPU_ERR_ARG if a run is longer than 16 (reported as
-   FD_ED25519_ERR_SIG for that run, like the reference's batch_sz>16). */
+   out_txn_code[t] is written for the t-th run (t < out_cap); returns the
+   run count (which may exceed out_cap: runs past it are counted, not
+   written).  A run longer than 16 is not an error of this call: its code is
+   FD_ED25519_ERR_SIG, like the reference's batch_sz > 16 (:238-240). */
 int64_t fd_ed25519_gpu_txn_reduce( int8_t const * out_code, fd_ed25519_desc_t const * desc, uint64_t n,
                                    int8_t * out_txn_code, uint64_t out_cap );
 

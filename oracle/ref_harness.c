@@ -18,9 +18,24 @@
      fd_ed25519_sign                     src/ballet/ed25519/fd_ed25519_user.c:59
      fd_ed25519_public_from_private      src/ballet/ed25519/fd_ed25519_user.c:4  */
 
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
 #include "ballet/ed25519/fd_ed25519.h"
 #include <pthread.h>
+#include <sched.h>
 #include <string.h>
+
+/* Pin the calling thread to one logical CPU (cpu < 0: leave it unpinned).
+   The CPU baselines run one thread per physical core (bench.py). */
+static void
+fdref_pin( int cpu ) {
+  if( cpu<0 ) return;
+  cpu_set_t set;
+  CPU_ZERO( &set );
+  CPU_SET( cpu, &set );
+  pthread_setaffinity_np( pthread_self(), sizeof(set), &set );
+}
 
 /* Descriptor layout shared with include/fd_ed25519_gpu.h (16 bytes). */
 typedef struct {
@@ -77,11 +92,13 @@ typedef struct {
   fdref_desc_t const * desc;
   ulong                lo, hi, passes;
   schar *              out;
+  int                  cpu;
 } fdref_job_t;
 
 static void *
 fdref_worker( void * _job ) {
   fdref_job_t * job = (fdref_job_t *)_job;
+  fdref_pin( job->cpu );
   fd_sha512_t _sha[1];
   fd_sha512_t * sha = fd_sha512_join( fd_sha512_new( _sha ) );
   for( ulong p=0UL; p<job->passes; p++ ) {
@@ -94,8 +111,10 @@ fdref_worker( void * _job ) {
   return NULL;
 }
 
+/* cpus: NULL (unpinned) or nthreads logical CPU ids, thread t pinned to cpus[t] */
 int
-fdref_verify_descs( uchar const * arena, void const * desc, ulong n, schar * out, ulong nthreads, ulong passes ) {
+fdref_verify_descs_pinned( uchar const * arena, void const * desc, ulong n, schar * out, ulong nthreads,
+                           ulong passes, int const * cpus ) {
   if( nthreads<1UL ) nthreads = 1UL;
   if( nthreads>256UL ) nthreads = 256UL;
   pthread_t   tid[ 256 ];
@@ -107,10 +126,16 @@ fdref_verify_descs( uchar const * arena, void const * desc, ulong n, schar * out
     job[ t ].hi     = (t+1UL)*n/nthreads;
     job[ t ].passes = passes;
     job[ t ].out    = out;
+    job[ t ].cpu    = cpus ? cpus[ t ] : -1;
     if( pthread_create( &tid[ t ], NULL, fdref_worker, &job[ t ] ) ) return -1;
   }
   for( ulong t=0UL; t<nthreads; t++ ) pthread_join( tid[ t ], NULL );
   return 0;
+}
+
+int
+fdref_verify_descs( uchar const * arena, void const * desc, ulong n, schar * out, ulong nthreads, ulong passes ) {
+  return fdref_verify_descs_pinned( arena, desc, n, out, nthreads, passes, NULL );
 }
 
 /* Multi-threaded SHA-512 sweep with the reference fd_sha512_hash
@@ -122,11 +147,13 @@ typedef struct {
   uint const *  msg;
   ulong         lo, hi, passes;
   uchar *       out;
+  int           cpu;
 } fdref_sha_job_t;
 
 static void *
 fdref_sha_worker( void * _job ) {
   fdref_sha_job_t * job = (fdref_sha_job_t *)_job;
+  fdref_pin( job->cpu );
   for( ulong p=0UL; p<job->passes; p++ )
     for( ulong i=job->lo; i<job->hi; i++ )
       fd_sha512_hash( job->arena + job->msg[ 2UL*i ], job->msg[ 2UL*i+1UL ], job->out + 64UL*i );
@@ -134,7 +161,8 @@ fdref_sha_worker( void * _job ) {
 }
 
 int
-fdref_sha512_msgs( uchar const * arena, void const * msg, ulong n, uchar * out, ulong nthreads, ulong passes ) {
+fdref_sha512_msgs_pinned( uchar const * arena, void const * msg, ulong n, uchar * out, ulong nthreads, ulong passes,
+                          int const * cpus ) {
   if( nthreads<1UL ) nthreads = 1UL;
   if( nthreads>256UL ) nthreads = 256UL;
   pthread_t       tid[ 256 ];
@@ -146,10 +174,16 @@ fdref_sha512_msgs( uchar const * arena, void const * msg, ulong n, uchar * out, 
     job[ t ].hi     = (t+1UL)*n/nthreads;
     job[ t ].passes = passes;
     job[ t ].out    = out;
+    job[ t ].cpu    = cpus ? cpus[ t ] : -1;
     if( pthread_create( &tid[ t ], NULL, fdref_sha_worker, &job[ t ] ) ) return -1;
   }
   for( ulong t=0UL; t<nthreads; t++ ) pthread_join( tid[ t ], NULL );
   return 0;
+}
+
+int
+fdref_sha512_msgs( uchar const * arena, void const * msg, ulong n, uchar * out, ulong nthreads, ulong passes ) {
+  return fdref_sha512_msgs_pinned( arena, msg, n, out, nthreads, passes, NULL );
 }
 
 /* ---- verify stage ------------------------

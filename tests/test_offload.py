@@ -176,3 +176,86 @@ def test_burst_publish_and_results(link):
     assert cli.results(0, res[:40], sig[:40]) == 16
     assert list(sig[:16]) == [_frag(i, 200)[1] for i in range(16)]
     assert cli.publish_burst(arena, fr[16:]) == 16
+
+
+# Header layout of fd_verify_offload.cpp (struct hdr): the geometry words,
+# then one 64-B line per cursor.
+_H_DEPTH, _H_DSZ, _H_FOOT, _H_FRAG, _H_RES, _H_SIG, _H_DC = 8, 16, 24, 32, 40, 48, 56
+_H_PROD, _H_CURSOR, _H_CONS, _H_DONE = 64, 72, 128, 192
+
+
+def _shm_u64(name):
+    """Writable u64 view of the link's first page, as another process (a
+    buggy or hostile client) would map it."""
+    import mmap
+    fd = os.open("/dev/shm" + name, os.O_RDWR)
+    m = mmap.mmap(fd, 4096)
+    os.close(fd)
+    return m
+
+
+def _put(m, off, v):
+    m[off:off + 8] = int(v).to_bytes(8, "little")
+
+
+def test_corrupt_header_cannot_move_server_out_of_bounds():
+    """the server must not take the ring geometry or its own
+    consumer cursor from the shared header after create.  A client that
+    rewrites depth / region offsets / cons_seq / prod_seq leaves the server
+    indexing inside its own validated ring."""
+    name = NAME + "_c"
+    srv = fa.OffloadLink.create(name, depth=16, dcache_sz=4096)
+    cli = fa.OffloadLink.join(name)
+    try:
+        for i in range(5):
+            assert cli.publish(_frag(i, 100)) == i
+        m = _shm_u64(name)
+        _put(m, _H_DEPTH, 1 << 40)            # geometry rewritten behind the server's back
+        _put(m, _H_DSZ, 1 << 40)
+        _put(m, _H_FRAG, 1 << 50)
+        _put(m, _H_RES, 1 << 50)
+        _put(m, _H_SIG, 1 << 50)
+        _put(m, _H_DC, 1 << 50)
+        _put(m, _H_CONS, 12345678)            # the server's cursor is private: this is ignored
+        assert srv.depth == 16 and srv.dcache_sz == 4096
+        first, n = srv.avail()
+        assert (first, n) == (0, 5)
+        got = fake_serve(srv, lambda b: (0, len(b)))
+        assert [g[2] for g in got] == [_frag(i, 100) for i in range(5)]
+        assert int.from_bytes(m[_H_CONS:_H_CONS + 8], "little") == 5   # published one way
+        # a client claiming far more in flight than the ring holds: capped at depth, ring-contiguous
+        _put(m, _H_PROD, 5 + (1 << 33))
+        first, n = srv.avail()
+        assert first == 5 and 0 < n <= 16 - (5 % 16)
+        _put(m, _H_PROD, 3)                    # prod behind cons: nothing available
+        assert srv.avail() == (5, 0)
+        # the client's own handle also keeps its validated geometry
+        assert cli.depth == 16 and cli.dcache_sz == 4096
+        m.close()
+    finally:
+        cli.close()
+        srv.close()
+
+
+@pytest.mark.parametrize("field,value", [
+    (_H_DEPTH, 24),                # not a power of two
+    (_H_DEPTH, 1 << 30),           # rings past the mapping
+    (_H_DSZ, 100),                 # not a multiple of 64
+    (_H_DSZ, 1 << 30),             # frag area past the mapping
+    (_H_FRAG, 1 << 40),
+    (_H_RES, 1 << 62),
+    (_H_SIG, 7),                   # misaligned / inside the header
+    (_H_DC, (1 << 64) - 64),       # offset + size wraps around
+])
+def test_join_refuses_bad_geometry(field, value):
+    name = NAME + "_g"
+    srv = fa.OffloadLink.create(name, depth=16, dcache_sz=4096)
+    try:
+        m = _shm_u64(name)
+        _put(m, field, value)
+        m.close()
+        with pytest.raises(fa.GpuError):
+            fa.OffloadLink.join(name)
+        assert srv.depth == 16         # the creator is unaffected
+    finally:
+        srv.close()

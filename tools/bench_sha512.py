@@ -6,8 +6,8 @@ Workload: --n messages (default 1,048,576) of --msg-sz bytes (default 200,
 the config-2 message size; 1232 = the txn MTU), random bytes, packed back to
 back (unaligned).  value = messages/s; also GB/s of message bytes and the
 kernel's average launch time (HIP events on the launch stream).  CPU
-baseline: the reference fd_sha512_hash (oracle/_ref, AVX2 core) on 16 host
-threads over a bounded sample."""
+baseline: the reference fd_sha512_hash (oracle/_ref, AVX2 core) on one pinned
+thread per physical host core over a bounded sample."""
 import argparse
 import ctypes
 import json
@@ -25,22 +25,27 @@ def cpu_baseline(arena, msg, out_len, budget_s=5.0):
     path = os.path.join(REPO, "oracle", "_ref", "libfdref_avx512.so")
     if not os.path.exists(path):
         return None
+    from firedancer_amd.hostcpu import baseline_cpus
+    cpus, topo = baseline_cpus()
+    threads = min(len(cpus), 256)
+    cpu_arr = (ctypes.c_int * threads)(*cpus[:threads])
     lib = ctypes.CDLL(path)
-    lib.fdref_sha512_msgs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
-                                      ctypes.c_ulong, ctypes.c_ulong]
+    lib.fdref_sha512_msgs_pinned.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                                             ctypes.c_ulong, ctypes.c_ulong, ctypes.c_void_p]
     m = min(len(msg), 65536)
     d = np.ascontiguousarray(msg[:m])
     out = np.zeros(64 * m, np.uint8)
     vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-    threads = min(16, os.cpu_count() or 1)
-    lib.fdref_sha512_msgs(vp(arena), vp(d), m, vp(out), threads, 1)
+    lib.fdref_sha512_msgs_pinned(vp(arena), vp(d), m, vp(out), threads, 1, cpu_arr)
     t0 = time.perf_counter(); done = 0
     while time.perf_counter() - t0 < budget_s:
-        lib.fdref_sha512_msgs(vp(arena), vp(d), m, vp(out), threads, 1)
+        lib.fdref_sha512_msgs_pinned(vp(arena), vp(d), m, vp(out), threads, 1, cpu_arr)
         done += m
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "msgs/s", "cores": threads, "kind": "reference",
-            "sample": "%d passes x %d messages (%.1f s), fd_sha512_hash, %d pthreads" % (done // m, m, dt, threads)}
+            "per_core": done / dt / threads, "topology": topo,
+            "sample": "%d passes x %d messages (%.1f s), fd_sha512_hash, %d pthreads pinned one per physical "
+                      "core" % (done // m, m, dt, threads)}
 
 
 def main():
