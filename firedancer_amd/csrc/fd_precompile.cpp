@@ -39,11 +39,12 @@ span_of( fd_ed25519_gpu_precompile_t const * in, fd_ed25519_gpu_span_t const * t
 
 static inline uint16_t rd16( uint8_t const * p ) { uint16_t v; memcpy( &v, p, 2 ); return v; }
 
-extern "C" int
-fd_ed25519_gpu_precompile_verify( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
-                                  fd_ed25519_gpu_precompile_t const * instr, uint64_t n,
-                                  fd_ed25519_gpu_span_t const * txn_instr, uint64_t txn_instr_cnt, int * out ) {
-  if( !ctx || (n && (!instr || !out)) || (!arena && arena_sz) ) return FD_ED25519_GPU_ERR_ARG;
+extern "C" int64_t
+fd_ed25519_gpu_precompile_walk( uint8_t const * arena, uint64_t arena_sz,
+                                fd_ed25519_gpu_precompile_t const * instr, uint64_t n,
+                                fd_ed25519_gpu_span_t const * txn_instr, uint64_t txn_instr_cnt,
+                                fd_ed25519_desc_t * desc, uint64_t desc_cap, uint64_t * first, int * tail ) {
+  if( (n && (!instr || !first || !tail)) || (!arena && arena_sz) || (txn_instr_cnt && !txn_instr) ) return FD_ED25519_GPU_ERR_ARG;
   if( arena_sz > 0xffffffffull ) return FD_ED25519_GPU_ERR_ARG;
   /* every span the walk may read must lie in the arena */
   for( uint64_t j=0; j<n; j++ ) {
@@ -53,11 +54,9 @@ fd_ed25519_gpu_precompile_verify( fd_ed25519_gpu_t * ctx, uint8_t const * arena,
   for( uint64_t k=0; k<txn_instr_cnt; k++ )
     if( (uint64_t)txn_instr[ k ].off + txn_instr[ k ].sz > arena_sz ) return FD_ED25519_GPU_ERR_ARG;
 
-  std::vector<fd_ed25519_desc_t> desc;
-  std::vector<uint64_t> first( n + 1u );      /* descriptors of instruction j: [first[j], first[j+1]) */
-  std::vector<int>      tail( n );            /* the error after its last descriptor, or 0 */
+  uint64_t nd = 0;
   for( uint64_t j=0; j<n; j++ ) {
-    first[ j ] = desc.size();
+    first[ j ] = nd;
     fd_ed25519_gpu_precompile_t const * in = &instr[ j ];
     uint8_t const * data = arena + in->data.off;
     uint64_t dsz = in->data.sz;
@@ -74,16 +73,30 @@ fd_ed25519_gpu_precompile_verify( fd_ed25519_gpu_t * ctx, uint8_t const * arena,
       if( (e = span_of( in, txn_instr, rd16( so + 2 ),  rd16( so + 0 ), 64u,  &s_at )) ||
           (e = span_of( in, txn_instr, rd16( so + 6 ),  rd16( so + 4 ), 32u,  &p_at )) ||
           (e = span_of( in, txn_instr, rd16( so + 12 ), rd16( so + 8 ), msz,  &m_at )) ) { tail[ j ] = e; break; }
-      fd_ed25519_desc_t d;
-      d.sig_off = (uint32_t)s_at; d.pub_off = (uint32_t)p_at; d.msg_off = (uint32_t)m_at;
-      d.msg_sz = msz; d.txn_idx = (uint16_t)j;
-      desc.push_back( d );
+      if( nd >= desc_cap ) return FD_ED25519_GPU_ERR_ARG;
+      fd_ed25519_desc_t * d = &desc[ nd++ ];
+      d->sig_off = (uint32_t)s_at; d->pub_off = (uint32_t)p_at; d->msg_off = (uint32_t)m_at;
+      d->msg_sz = msz; d->txn_idx = (uint16_t)j;
     }
   }
-  first[ n ] = desc.size();
-  std::vector<int8_t> code( desc.size() ? desc.size() : 1u );
-  if( !desc.empty() ) {
-    int err = fd_ed25519_verify_batch_gpu( ctx, arena, arena_sz, desc.data(), desc.size(), code.data() );
+  if( n ) first[ n ] = nd;
+  return (int64_t)nd;
+}
+
+extern "C" int
+fd_ed25519_gpu_precompile_verify( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                                  fd_ed25519_gpu_precompile_t const * instr, uint64_t n,
+                                  fd_ed25519_gpu_span_t const * txn_instr, uint64_t txn_instr_cnt, int * out ) {
+  if( !ctx || (n && (!instr || !out)) ) return FD_ED25519_GPU_ERR_ARG;
+  std::vector<fd_ed25519_desc_t> desc( 255u * n + 1u );
+  std::vector<uint64_t> first( n + 1u );      /* descriptors of instruction j: [first[j], first[j+1]) */
+  std::vector<int>      tail( n + 1u );       /* the error after its last descriptor, or 0 */
+  int64_t nd = fd_ed25519_gpu_precompile_walk( arena, arena_sz, instr, n, txn_instr, txn_instr_cnt,
+                                               desc.data(), desc.size(), first.data(), tail.data() );
+  if( nd < 0 ) return (int)nd;
+  std::vector<int8_t> code( nd ? (size_t)nd : 1u );
+  if( nd ) {
+    int err = fd_ed25519_verify_batch_gpu( ctx, arena, arena_sz, desc.data(), (uint64_t)nd, code.data() );
     if( err ) return err;
   }
   for( uint64_t j=0; j<n; j++ ) {

@@ -59,6 +59,8 @@ def load_lib():
     vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
     lib.fd_ed25519_gpu_new.restype = vp
     lib.fd_ed25519_gpu_new.argtypes = [u64, u64]
+    lib.fd_ed25519_gpu_new_devs.restype = vp
+    lib.fd_ed25519_gpu_new_devs.argtypes = [vp, i32, u64]
     lib.fd_ed25519_gpu_delete.argtypes = [vp]
     lib.fd_ed25519_gpu_device_cnt.argtypes = [vp]
     lib.fd_ed25519_gpu_set_codes.argtypes = [vp, i32]
@@ -145,11 +147,17 @@ def txn_reduce(codes, desc):
 
 
 class Ed25519Gpu:
-    """One verify context (fd_ed25519_gpu_t) over the GPUs in device_mask."""
+    """One verify context (fd_ed25519_gpu_t) over the GPUs in device_mask, or
+    over an explicit list of shard slots (devices=[0, 0] = two slots on GPU 0:
+    fd_ed25519_gpu_new_devs)."""
 
-    def __init__(self, device_mask=0, max_batch=1 << 18, codes=CODES_AVX512):
+    def __init__(self, device_mask=0, max_batch=1 << 18, codes=CODES_AVX512, devices=None):
         self.lib = load_lib()
-        self.ctx = self.lib.fd_ed25519_gpu_new(device_mask, max_batch)
+        if devices is not None:
+            ids = (ctypes.c_int * len(devices))(*devices)
+            self.ctx = self.lib.fd_ed25519_gpu_new_devs(ids, len(devices), max_batch)
+        else:
+            self.ctx = self.lib.fd_ed25519_gpu_new(device_mask, max_batch)
         if not self.ctx:
             raise GpuError("fd_ed25519_gpu_new failed (no HIP device?)")
         self.set_codes(codes)

@@ -325,6 +325,20 @@ int fd_ed25519_gpu_precompile_verify( fd_ed25519_gpu_t * ctx, uint8_t const * ar
                                       fd_ed25519_gpu_span_t const * txn_instr, uint64_t txn_instr_cnt,
                                       int * out );
 
+/* Its host half (no GPU; the record walk over attacker-shaped instruction
+   data): every instruction's records in order up to its first size /
+   offsets error, one descriptor per signature before it (txn_idx = the
+   instruction index).  first[j] = index of instruction j's first descriptor
+   (first[n] = the total, n + 1 entries), tail[j] = the walk's error after
+   them or 0.  desc holds desc_cap entries; at most 255 per instruction are
+   emitted (data[0] is the count), so desc_cap = 255 n always suffices.
+   Returns the descriptor count, or FD_ED25519_GPU_ERR_ARG (a span outside
+   the arena, or desc_cap too small; nothing is guaranteed written then). */
+int64_t fd_ed25519_gpu_precompile_walk( uint8_t const * arena, uint64_t arena_sz,
+                                        fd_ed25519_gpu_precompile_t const * instr, uint64_t n,
+                                        fd_ed25519_gpu_span_t const * txn_instr, uint64_t txn_instr_cnt,
+                                        fd_ed25519_desc_t * desc, uint64_t desc_cap, uint64_t * first, int * tail );
+
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
    u32 words each, k < l) on the context's first device.  out: n records of

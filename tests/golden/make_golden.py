@@ -23,6 +23,17 @@ Files written (tests/golden/):
                     variable-length messages 0..1232 B (set 11)
   txn_batches.bin   multi-signature single-message batches (A2 precedence)
   sha512_kat.bin    SHA-512 known answers (fd_sha512_test_vector.c + CAVP ShortMsg/LongMsg)
+  cctv_batches.bin  the reference's own batch scenario, test_cctv_batch
+                    (src/ballet/ed25519/test_ed25519.c:1041-1082): 16 fresh valid
+                    signatures over CCTV message #7, then each CCTV vector with that
+                    message at slot 1 of 2- and 4-signature batches (txn format; the
+                    reference's `ok` re-asserted on the batch codes)
+  fuzz_seeds.bin    the 4 corpus/fuzz_ed25519_sigverify seeds through the harness of
+                    src/ballet/ed25519/fuzz_ed25519_sigverify.c:30-49 (seed = prv[32] || msg:
+                    public_from_private, sign, verify must be SUCCESS), as sig records
+                    (set 50), reference codes recorded
+
+`python3 make_golden.py cctv_batches.bin fuzz_seeds.bin` rewrites only the named files.
 
 Record format (ed25519 files), little endian:
   u32 set, u32 tc_id, i8 code_avx512, i8 code_ref, i8 ok, u8 0, u32 msg_sz,
@@ -278,6 +289,52 @@ def gen_txn_batches():
     return out
 
 
+def gen_cctv_batches(vecs):
+    """test_cctv_batch (test_ed25519.c:1041-1082) as fixtures: the reference
+    draws the 16 keys from fd_rng(seed 0); any 16 fresh keys exercise the same
+    scenario, so ours come from a fixed numpy seed and the reference signer."""
+    cctv = [v for v in vecs if v[0] == 2]
+    msg = cctv[7][3]
+    rng = np.random.default_rng(1041)
+    sigs, pubs = [], []
+    for _ in range(16):
+        priv, pub = keypair(rng)
+        sigs.append(sign(msg, pub, priv)); pubs.append(pub)
+    assert verify_batch(msg, b"".join(sigs), b"".join(pubs), 16) == (0, 0)     # :1057
+    out = []
+    for set_id, tc_id, ok, m, sig, pub in cctv:
+        if m != msg:
+            continue
+        s2 = list(sigs); p2 = list(pubs)
+        s2[1] = sig; p2[1] = pub                                                   # :1069-1070
+        for n in (2, 4):                                                           # :1072, :1076
+            sb = b"".join(s2[:n]); pb = b"".join(p2[:n])
+            codes = verify_batch(msg, sb, pb, n)
+            if ok in (0, 1):
+                assert (codes[0] == 0) == bool(ok), (tc_id, n, codes, ok)
+            out.append(struct.pack("<IIbbH", n, len(msg), codes[0], codes[1], tc_id & 0xffff) + sb + pb + msg)
+    return out
+
+
+def gen_fuzz_seeds():
+    """corpus/fuzz_ed25519_sigverify/* through LLVMFuzzerTestOneInput
+    (fuzz_ed25519_sigverify.c:30-49): input = prv[32] || msg."""
+    d = os.path.join(os.path.dirname(REF_SRC), "corpus", "fuzz_ed25519_sigverify")
+    out = []
+    for i, name in enumerate(sorted(os.listdir(d))):
+        data = open(os.path.join(d, name), "rb").read()
+        if len(data) < 32:                      # :31 returns early
+            continue
+        priv, msg = data[:32], data[32:]
+        pub = ctypes.create_string_buffer(32)
+        LIBS["avx512"].fdref_public_from_private(pub, priv)
+        sig = sign(msg, pub.raw, priv)
+        codes = verify(msg, sig, pub.raw)
+        assert codes == (0, 0), (name, codes)  # :46-47
+        out.append(rec(50, i, codes, 1, msg, sig, pub.raw))
+    return out
+
+
 def gen_sha512(vecs):
     out = []
     for set_id, tc_id, ok, msg, sig, pub in vecs:
@@ -305,8 +362,12 @@ def main():
     global LIBS
     LIBS = load_libs()
     vecs = extract_reference_vectors()
-    for name, recs in (("vectors_ref.bin", gen_vectors_ref(vecs)), ("synthetic.bin", gen_synthetic()),
-                       ("txn_batches.bin", gen_txn_batches()), ("sha512_kat.bin", gen_sha512(vecs))):
+    gens = {"vectors_ref.bin": lambda: gen_vectors_ref(vecs), "synthetic.bin": gen_synthetic,
+            "txn_batches.bin": gen_txn_batches, "sha512_kat.bin": lambda: gen_sha512(vecs),
+            "cctv_batches.bin": lambda: gen_cctv_batches(vecs), "fuzz_seeds.bin": gen_fuzz_seeds}
+    only = sys.argv[1:] or list(gens)
+    for name in only:
+        recs = gens[name]()
         with open(os.path.join(HERE, name), "wb") as f:
             f.write(b"".join(recs))
         print(name, len(recs), "records", file=sys.stderr)

@@ -143,3 +143,28 @@ def test_shard_ranges_cover_exactly():
             rs = [shard_range(n, i, parts) for i in range(parts)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(parts - 1))
+
+
+def test_txn_reduce_long_run_is_err_sig_not_an_error():
+    """fd_ed25519_gpu_txn_reduce (host function, no GPU): a run of 17
+    descriptors of one txn is reported as FD_ED25519_ERR_SIG for that txn,
+    like the reference's batch_sz > 16 (fd_ed25519_user.c:238-240), and the
+    call returns the run count, not an error (include/fd_ed25519_gpu.h)."""
+    import numpy as np
+    import firedancer_amd as fa
+    desc = np.zeros(17 + 3 + 16, fa.DESC_DTYPE)
+    desc["txn_idx"][:17] = 5
+    desc["txn_idx"][17:20] = 6
+    desc["txn_idx"][20:] = 7
+    codes = np.zeros(len(desc), np.int8)
+    codes[18] = fa.FD_ED25519_ERR_MSG
+    codes[19] = fa.FD_ED25519_ERR_PUBKEY
+    codes[35] = fa.FD_ED25519_ERR_MSG
+    out = fa.txn_reduce(codes, desc)
+    assert list(out) == [fa.FD_ED25519_ERR_SIG, fa.FD_ED25519_ERR_PUBKEY, fa.FD_ED25519_ERR_MSG]
+    lib = fa.load_lib()
+    small = np.zeros(1, np.int8)
+    import ctypes
+    t = lib.fd_ed25519_gpu_txn_reduce(codes.ctypes.data_as(ctypes.c_void_p), desc.ctypes.data_as(ctypes.c_void_p),
+                                      len(desc), small.ctypes.data_as(ctypes.c_void_p), 1)
+    assert t == 3 and small[0] == fa.FD_ED25519_ERR_SIG      # runs past out_cap are counted, not written

@@ -9,7 +9,7 @@ import pytest
 from golden_io import read_sha, read_sigs, read_txns
 
 
-@pytest.mark.parametrize("fname", ["vectors_ref.bin", "synthetic.bin"])
+@pytest.mark.parametrize("fname", ["vectors_ref.bin", "synthetic.bin", "fuzz_seeds.bin"])
 def test_oracle_codes_bit_exact(oracle, fname):
     recs = read_sigs(fname)
     assert recs
@@ -33,8 +33,9 @@ def test_golden_distribution_matches_survey():
     assert hist(5, "code") == {0: 200}
 
 
-def test_oracle_txn_batches(oracle):
-    for r in read_txns():
+@pytest.mark.parametrize("fname", ["txn_batches.bin", "cctv_batches.bin"])
+def test_oracle_txn_batches(oracle, fname):
+    for r in read_txns(fname):
         sigs = b"".join(r["sigs"]) or bytes(64)
         pubs = b"".join(r["pubs"]) or bytes(32)
         for fl, exp in ((0, r["code"]), (1, r["code_ref"])):
@@ -49,3 +50,19 @@ def test_oracle_sha512_kat(oracle):
         oracle.fdo_sha512(m, len(m), out)
         assert out.raw == md
         assert hashlib.sha512(m).digest() == md
+
+
+def test_reference_scenarios_present():
+    """test_cctv_batch (test_ed25519.c:1041-1082): every CCTV vector over
+    message #7 at slot 1 of a 2- and a 4-signature batch, accept/reject as the
+    reference test asserts; the 4 fuzz corpus seeds sign+verify to SUCCESS."""
+    cb = read_txns("cctv_batches.bin")
+    assert len(cb) == 206 and {r["n"] for r in cb} == {2, 4}
+    cctv7 = [r for r in read_sigs("vectors_ref.bin") if r["set"] == 2 and r["msg"] == cb[0]["msg"]]
+    assert len(cctv7) == 103
+    for i, v in enumerate(cctv7):
+        for r in cb[2 * i:2 * i + 2]:
+            assert r["sigs"][1] == v["sig"] and r["pubs"][1] == v["pub"]
+            assert (r["code"] == 0) == (v["ok"] == 1)
+    fz = read_sigs("fuzz_seeds.bin")
+    assert len(fz) == 4 and all(r["code"] == 0 and r["code_ref"] == 0 for r in fz)
