@@ -16,7 +16,9 @@ _OLIB = None
 
 
 def offload_lib_path():
-    return os.path.join(_HERE, "libfd_verify_offload.so")
+    """The in-tree link library; FD_VERIFY_OFFLOAD_LIB may name a test build
+    of the same source (tests/csrc/Makefile asan: ASan + UBSan)."""
+    return os.environ.get("FD_VERIFY_OFFLOAD_LIB") or os.path.join(_HERE, "libfd_verify_offload.so")
 
 
 def server_path():
