@@ -211,6 +211,9 @@ def main():
                     help="untimed back-to-back steps for this long before the warm-up steps: a GPU that was idle "
                          "runs its first ~100 ms at a ramping clock; the timed region should see the clock a "
                          "continuously fed verify stage runs at (reported as prime_steps)")
+    ap.add_argument("--pipeline", type=int, default=0, choices=[0, 1],
+                    help="1: each step is one fd_ed25519_gpu_pipe_dev launch (this batch's first phase beside the "
+                         "previous batch's second phase: two batches in flight, every launch one batch of work)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test mode (tests/test_bench_launch.py): gloo, a no-op step on a fixed count; "
                          "exercises the launcher, rank setup and SUM/MAX aggregation without a GPU")
@@ -267,10 +270,26 @@ def main():
     d_out = torch.zeros(n, dtype=torch.int8, device=dev)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
+    pipe = bool(args.pipeline) and not args.hot_keys and n <= 65536 * 4
+    d_outs = [d_out, torch.zeros(n, dtype=torch.int8, device=dev)]
+    nstep = [0]
 
     def step():
+        if pipe:   # batch i's codes land in d_outs[i % 2] when launch i+1 completes
+            g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, d_outs[nstep[0] & 1].data_ptr(),
+                       stream=stream.cuda_stream)
+            nstep[0] += 1
+            return
         g.verify_batch_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, d_out.data_ptr(),
                            stream=stream.cuda_stream)
+
+    def settle():
+        """codes of every launched batch final (pipeline: the pending second phase)"""
+        if pipe:
+            g.pipe_flush_dev(stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        for o in (d_outs if pipe else [d_out]):
+            assert np.array_equal(o.cpu().numpy(), expect), "verify codes differ from the expected ones"
 
     prime = 0
     t_prime = time.perf_counter()
@@ -282,7 +301,6 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    assert np.array_equal(d_out.cpu().numpy(), expect), "verify codes differ from the expected ones"
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     barrier()
@@ -296,7 +314,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    assert np.array_equal(d_out.cpu().numpy(), expect)
+    settle()
 
     from firedancer_amd.dist import aggregate_throughput
     total, dt_max = aggregate_throughput(n * args.steps, dt, device=dev)
@@ -331,6 +349,10 @@ def main():
             "cpu_baseline": None,
             "prime_steps": prime,
         }
+        if pipe:
+            line["pipeline"] = ("fd_ed25519_gpu_pipe_dev: each timed step is one launch running this batch's first "
+                                "phase (checks, SHA-512, lattice, decodes, tables) beside the previous batch's second "
+                                "phase (chain, compare); two batches in flight, every launch one batch of work")
         # The same launch against the HBM roofline (not the bound: ~1/6 of the ~8 TB/s peak),
         # from the PMC-measured bytes per launch of profiles/r01/pmc_traffic.json.
         t = pmc_traffic(n) if args.config == 2 and not args.hot_keys else None

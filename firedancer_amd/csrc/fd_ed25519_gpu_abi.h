@@ -65,6 +65,32 @@ struct verify_args {
   uint64_t                  kcap;      /* slots */
 };
 
+/* Pipelined verify (fd_ed25519_verify_pipe_kernel): one launch runs the
+   first phase (checks, SHA-512, lattice, digits, decode and table of A) of
+   batch "cur" beside the second phase (decode and table of R, the final
+   check-order code, the scalar multiplication and compare) of the previous
+   batch "prev", whose first phase ran in the previous launch.  Between the
+   two phases a batch lives in HBM: its tables in set s of the pipe table
+   scratch (A of slot g at table 2 s sig_cap + g, R at (2 s + 1) sig_cap + g;
+   v.vtab_cap = 4 sig_cap), its digit rows (FD_ROWS rows of sig_cap bytes,
+   the LDS row layout) and its partial status per slot (FD_PIPE_ST_* bits,
+   fd_ed25519_gpu_kern.hip); the previous batch's arena and descriptors are
+   read again for R. */
+struct pipe_args {
+  verify_args               v;          /* arena, arena_sz, desc, n (= cur count), ctab, vtab, vtab_cap, ref_codes */
+  uint64_t                  sig_cap;    /* slots per table set / digit rows */
+  uint64_t                  set_cur;    /* 0 / 1: cur writes set_cur, prev is read from set_cur ^ 1 */
+  uint8_t *                 dig_cur;    /* FD_ROWS x sig_cap */
+  int8_t *                  pcode_cur;  /* sig_cap */
+  uint8_t const *           dig_prev;
+  int8_t const *            pcode_prev;
+  uint64_t                  n_prev;     /* 0: no previous batch */
+  int8_t *                  out_prev;   /* codes of the previous batch */
+  uint8_t const *           arena_prev; /* the previous batch's arena and descriptors (R is decoded from them) */
+  uint64_t                  arena_sz_prev;
+  fd_ed25519_desc_t const * desc_prev;
+};
+
 struct kpart_args {
   uint8_t const *           arena;
   uint64_t                  arena_sz;
@@ -114,6 +140,7 @@ struct fparse_args {
 #define FD_KERN_FSCAN    "fd_frag_scan_kernel"
 #define FD_KERN_FEMIT    "fd_frag_emit_kernel"
 #define FD_KERN_FFOLD    "fd_frag_fold_kernel"
+#define FD_KERN_PIPE     "fd_ed25519_verify_pipe_kernel"
 
 /* Seeded key hash shared by the host (slot assignment) and the device
    (lookup): splitmix64 of the key's first 8 bytes xor seed. */

@@ -339,7 +339,7 @@ __device__ __forceinline__ int bitlen8( uint32_t const x[ 8 ] ) {
 /* Signed 4-bit recoding of x (< 2^(4 nw - 1)) into nw LDS rows (biased by 8,
    negated when neg): digits in [-8, 7] below the top one, top digit in
    [0, 8] (its top nibble <= 7 plus the incoming carry, never wrapped). */
-__device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 ], int neg, int nw ) {
+__device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 ], int neg, int nw, uint64_t stride ) {
   int c = 0;
 #pragma unroll
   for( int i=0; i<FD_NDIG_MAX; i++ ) {
@@ -347,16 +347,18 @@ __device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 
       int d = (int)((x[i>>3] >> (4*(i&7))) & 15u) + c;
       c = d >= 8 && i < nw-1;           /* the top digit keeps its carry: d in [0, 8] */
       d -= c << 4;
-      row[ i*FD_VERIFY_BLOCK ] = (uint8_t)((neg ? -d : d) + 8);
+      row[ (uint64_t)i*stride ] = (uint8_t)((neg ? -d : d) + 8);
     }
   }
 }
 
 /* k = SHA-512(R||A||M) mod l, the lattice vector (u, v), w = v S mod l, and
-   their digits into this lane's LDS column drow (rows FD_ROW_U / _V / _W;
-   FD_ROW_NW of lane 0: the wave-uniform window count).  Lanes that are not
-   live write zero digits (every lane takes part in the wave max). */
-__device__ __forceinline__ void verify_prep_digits( uint8_t * drow, int tid, bool live, uint32_t const sig[ 16 ],
+   their digits into this lane's column drow (rows FD_ROW_U / _V / _W, row r
+   at drow[r * stride]: LDS with stride FD_VERIFY_BLOCK, or the pipelined
+   kernel's HBM rows; FD_ROW_NW: the wave-uniform window count, written by
+   lane 0 of each wave).  Lanes that are not live write zero digits (every
+   lane takes part in the wave max). */
+__device__ __forceinline__ void verify_prep_digits( uint8_t * drow, uint64_t stride, int tid, bool live, uint32_t const sig[ 16 ],
                                                     uint32_t const pub[ 8 ], verify_args const & args,
                                                     fd_ed25519_desc_t const & d, uint32_t lim_dw
 #ifdef FD_PHASE_STAMPS
@@ -394,8 +396,8 @@ __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, int tid, boo
       int dd = (int)((w[k>>1] >> (16*(k&1))) & 0xffffu) + c;
       c = dd >= 32768 && k < FD_CTAB_POS-1;
       dd -= c << 16;
-      drow[ (FD_ROW_W + 2*k    )*FD_VERIFY_BLOCK ] = (uint8_t)(dd & 255);
-      drow[ (FD_ROW_W + 2*k + 1)*FD_VERIFY_BLOCK ] = (uint8_t)((dd >> 8) & 255);
+      drow[ (uint64_t)(FD_ROW_W + 2*k    )*stride ] = (uint8_t)(dd & 255);
+      drow[ (uint64_t)(FD_ROW_W + 2*k + 1)*stride ] = (uint8_t)((dd >> 8) & 255);
     }
     nbits = max( bitlen8( u ), bitlen8( v ) );
   }
@@ -403,23 +405,15 @@ __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, int tid, boo
 #pragma unroll
   for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
   int nw = min( FD_NDIG_MAX, max( 32, (nbits + 4) >> 2 ) );
-  recode4_lds( drow + FD_ROW_U*FD_VERIFY_BLOCK, u, un, nw );
-  recode4_lds( drow + FD_ROW_V*FD_VERIFY_BLOCK, v, 0,  nw );
-  if( (tid & 63) == 0 ) drow[ FD_ROW_NW*FD_VERIFY_BLOCK ] = (uint8_t)nw;
+  recode4_lds( drow + FD_ROW_U*stride, u, un, nw, stride );
+  recode4_lds( drow + FD_ROW_V*stride, v, 0,  nw, stride );
+  if( (tid & 63) == 0 ) drow[ FD_ROW_NW*stride ] = (uint8_t)nw;
   }
 
 /* The verify code from the check results, in the reference's order
-   (fd_ed25519_user.c:157-228), and for lanes still at 0 the equation:
-   Q = [u](-A) + [v](-R) + [w]B (tables at vtab[gid] / vtab[cap/2 + gid],
-   digits in LDS) and Q == O. */
-__device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_ok, bool bad_s, int stA, int stR,
-                                            uint8_t const * drow, uint8_t const * s_dig, int tid, uint64_t gid,
-                                            uint32_t const * s_wb  /* NULL: add [w]B here; else its cached form in LDS ([word][256]) */
-#ifdef FD_PHASE_STAMPS
-                                            , uint64_t * _st
-#endif
-                                            ) {
-  uint64_t cap = args.vtab_cap;
+   (fd_ed25519_user.c:157-228): 0 means every check before the equation
+   passed. */
+__device__ __forceinline__ int verify_precode( verify_args const & args, bool desc_ok, bool bad_s, int stA, int stR ) {
   int code;
   if     ( !desc_ok    ) code = FD_ED25519_GPU_CODE_BAD_DESC;
   else if( bad_s       ) code = FD_ED25519_ERR_SIG;
@@ -428,31 +422,59 @@ __device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_
   else if( stA & 2     ) code = FD_ED25519_ERR_PUBKEY;                                        /* :193-195 */
   else if( stR & 2     ) code = FD_ED25519_ERR_SIG;                                           /* :196-198 */
   else                   code = 0;
+  return code;
+}
 
-  if( code == 0 ) {
-    int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
-    ge_p3 acc;
-    if( !s_wb ) dsm_loop<true>( acc, args.vtab, cap, gid, cap/2u + gid, drow, args.ctab, nw );
-    else {
-      dsm_loop<false>( acc, args.vtab, cap, gid, cap/2u + gid, drow, args.ctab, nw );
-      ge_cached c;
+/* The equation for a lane whose checks passed: Q = [u](-A) + [v](-R) + [w]B
+   (tables ta / tr of vtab, digits in this lane's LDS column drow, the
+   wave's window count in s_dig) and Q == O -> SUCCESS / ERR_MSG. */
+__device__ __forceinline__ int verify_equation( verify_args const & args, uint8_t const * drow, uint8_t const * s_dig,
+                                                int tid, uint64_t ta, uint64_t tr,
+                                                uint32_t const * s_wb  /* NULL: add [w]B here; else its cached form in LDS ([word][256]) */
+#ifdef FD_PHASE_STAMPS
+                                                , uint64_t * _st
+#endif
+                                                ) {
+  uint64_t cap = args.vtab_cap;
+  int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
+  ge_p3 acc;
+  if( !s_wb ) dsm_loop<true>( acc, args.vtab, cap, ta, tr, drow, args.ctab, nw );
+  else {
+    dsm_loop<false>( acc, args.vtab, cap, ta, tr, drow, args.ctab, nw );
+    ge_cached c;
 #pragma unroll
-      for( int j=0; j<10; j++ ) {
-        c.YpX.v[j] = s_wb[ (j     )*FD_VERIFY_BLOCK + tid ]; c.YmX.v[j] = s_wb[ (10 + j)*FD_VERIFY_BLOCK + tid ];
-        c.T2d.v[j] = s_wb[ (20 + j)*FD_VERIFY_BLOCK + tid ]; c.Z2.v[j]  = s_wb[ (30 + j)*FD_VERIFY_BLOCK + tid ];
-      }
-      FE_FENCE();
-      ge_add_cached( acc, acc, c, false );
-      FE_FENCE();
+    for( int j=0; j<10; j++ ) {
+      c.YpX.v[j] = s_wb[ (j     )*FD_VERIFY_BLOCK + tid ]; c.YmX.v[j] = s_wb[ (10 + j)*FD_VERIFY_BLOCK + tid ];
+      c.T2d.v[j] = s_wb[ (20 + j)*FD_VERIFY_BLOCK + tid ]; c.Z2.v[j]  = s_wb[ (30 + j)*FD_VERIFY_BLOCK + tid ];
     }
-    STAMP( 5 );
-    /* Q == O  <=>  X == 0 and Y == Z (the reference's projective compare, :225-228, on [v]D) */
-    fe dl;
-    int ex = fe_is_zero( acc.X );
-    fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
-    int ey = fe_is_zero( dl );
-    code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+    FE_FENCE();
+    ge_add_cached( acc, acc, c, false );
+    FE_FENCE();
   }
+  STAMP( 5 );
+  /* Q == O  <=>  X == 0 and Y == Z (the reference's projective compare, :225-228, on [v]D) */
+  fe dl;
+  int ex = fe_is_zero( acc.X );
+  fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
+  int ey = fe_is_zero( dl );
+  return (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+/* The verify code: the checks, then for lanes at 0 the equation
+   (tables at vtab[gid] / vtab[cap/2 + gid]). */
+__device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_ok, bool bad_s, int stA, int stR,
+                                            uint8_t const * drow, uint8_t const * s_dig, int tid, uint64_t gid,
+                                            uint32_t const * s_wb
+#ifdef FD_PHASE_STAMPS
+                                            , uint64_t * _st
+#endif
+                                            ) {
+  int code = verify_precode( args, desc_ok, bad_s, stA, stR );
+  if( code == 0 ) code = verify_equation( args, drow, s_dig, tid, gid, args.vtab_cap/2u + gid, s_wb
+#ifdef FD_PHASE_STAMPS
+                                          , _st
+#endif
+                                          );
   return code;
 }
 
@@ -506,7 +528,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
 
   /* k, lattice vector, w and digits (before the decodes: only digits stay live) */
   uint8_t * drow = s_dig + tid;
-  verify_prep_digits( drow, tid, live, sig, pub, args, d, lim_dw
+  verify_prep_digits( drow, FD_VERIFY_BLOCK, tid, live, sig, pub, args, d, lim_dw
 #ifdef FD_PHASE_STAMPS
                       , _st
 #endif
@@ -607,7 +629,7 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
   uint8_t * drow = s_dig + tid;
 
   if( !role && wave_live ) {
-    verify_prep_digits( drow, tid, live, sig, pub, args, d, lim_dw
+    verify_prep_digits( drow, FD_VERIFY_BLOCK, tid, live, sig, pub, args, d, lim_dw
 #ifdef FD_PHASE_STAMPS
                         , nullptr
 #endif
@@ -653,6 +675,158 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
 #endif
                           );
   args.out[ gid ] = (int8_t)code;
+}
+
+/* Pipelined form (throughput): one launch runs the first phase of batch
+   "cur" and the second phase of the batch before it, in the two halves of
+   512-thread workgroups that share nothing (different batches: a batch's
+   A tables, digits and partial status cross the launch boundary in HBM,
+   pipe_args), so there is no barrier:
+     waves 0-3 (role 0, priority 3), previous batch: decode R, small-order R,
+       R's table, the final check-order code, then for lanes still passing
+       the Straus chain + [w]B + the compare;
+     waves 4-7 (role 1), current batch: descriptor / S checks, SHA-512,
+       lattice, digits, decode A, small-order A, A's table.
+   Why: one 64-signature wave per SIMD leaves VALU issue slots empty during
+   the chain; a second wave of independent work fills them without slowing
+   the first (tools/fe_probe2.hip mix probe: a doubling wave at priority 3
+   keeps its 3,854 cycles per doubling beside 1-3 squaring waves, which get
+   0.1-0.2 instructions per cycle).  The split balances the two: role 0 runs
+   at ~0.24 VALU instructions per cycle, role 1 on the leftover ~0.08, so
+   role 0 takes the larger share (R's decode and table, ~31 K instructions,
+   moved over: the first version with both decodes in role 1 left role 1 at
+   1.35 M cycles per wave against role 0's 1.05 M).  Same device functions
+   and check order as fd_ed25519_verify_kernel: bit-identical codes. */
+#define FD_PIPE_ST_VALID  0x80      /* partial status of the first phase (pcode byte) */
+#define FD_PIPE_ST_DESC   0x01      /* descriptor inside the arena   */
+#define FD_PIPE_ST_BADS   0x02      /* S >= l                        */
+#define FD_PIPE_ST_A_OK   0x04      /* A decodes                     */
+#define FD_PIPE_ST_A_SM   0x08      /* A has small order             */
+extern "C" __global__ void __launch_bounds__( 2 * FD_VERIFY_BLOCK, 1 )
+fd_ed25519_verify_pipe_kernel( pipe_args a ) {
+  __shared__ uint8_t s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
+  int role = (int)threadIdx.x >> 8;                  /* wave-uniform */
+  int tid  = (int)threadIdx.x & (FD_VERIFY_BLOCK - 1);
+  uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)tid;
+  uint64_t cap = a.sig_cap;
+  verify_args const & args = a.v;
+
+  if( role == 0 ) {
+    /* ---- second phase of the previous batch ---- */
+    uint64_t np = a.n_prev;
+    if( (gid & ~(uint64_t)63) >= np ) return;        /* whole waves past it */
+    __builtin_amdgcn_s_setprio( 3 );
+#ifdef FD_PHASE_STAMPS
+    uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
+    bool valid = gid < np;
+    int ps = valid ? (int)(uint8_t)a.pcode_prev[ gid ] : 0;
+    bool desc_ok = (ps & FD_PIPE_ST_DESC) != 0, bad_s = (ps & FD_PIPE_ST_BADS) != 0;
+    int stA = ((ps & FD_PIPE_ST_A_OK) ? 1 : 0) | ((ps & FD_PIPE_ST_A_SM) ? 2 : 0);
+    uint64_t sp = a.set_cur ^ 1u;
+    /* R = sig[0:32] of the previous batch: decode, small order, table */
+    int stR = 0;
+    if( desc_ok && !bad_s ) {
+      fd_ed25519_desc_t d = a.desc_prev[ gid ];
+      uint32_t lim_dw = (uint32_t)((a.arena_sz_prev + 3u) >> 2) + 1u;
+      uint32_t enc[ 8 ];
+      load_words<8>( enc, a.arena_prev, d.sig_off, lim_dw );
+      ge_p3 Q;
+      int ok = ge_decode( Q, enc, !args.ref_codes );
+      int sm = ge_affine_small_order( Q );
+      FE_FENCE();
+      if( ok && !sm && (stA & 1) && !(stA & 2) ) vtab_build( args.vtab, args.vtab_cap, (2u*sp + 1u)*cap + gid, Q );
+      stR = (ok ? 1 : 0) | (sm ? 2 : 0);
+      FE_FENCE();
+    }
+    int code = verify_precode( args, desc_ok, bad_s, stA, stR );
+    /* this lane's digit column from the HBM rows into its LDS column */
+    uint8_t * drow = s_dig + tid;
+    uint8_t const * g = a.dig_prev + gid;
+    int nw = (int)g[ (uint64_t)FD_ROW_NW * cap - (uint64_t)(tid & 63) ];   /* lane 0 of the wave wrote it */
+    nw = __builtin_amdgcn_readfirstlane( nw );
+    if( (tid & 63) == 0 ) drow[ FD_ROW_NW*FD_VERIFY_BLOCK ] = (uint8_t)nw;
+    bool run = valid && code == 0;
+    if( run ) {
+#pragma unroll 4
+      for( int i=0; i<nw; i++ ) {
+        drow[ (FD_ROW_U + i)*FD_VERIFY_BLOCK ] = g[ (uint64_t)(FD_ROW_U + i) * cap ];
+        drow[ (FD_ROW_V + i)*FD_VERIFY_BLOCK ] = g[ (uint64_t)(FD_ROW_V + i) * cap ];
+      }
+#pragma unroll 8
+      for( int i=0; i<2*FD_CTAB_POS; i++ ) drow[ (FD_ROW_W + i)*FD_VERIFY_BLOCK ] = g[ (uint64_t)(FD_ROW_W + i) * cap ];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if( run )
+      code = verify_equation( args, drow, s_dig, tid, (2u*sp)*cap + gid, (2u*sp + 1u)*cap + gid, nullptr
+#ifdef FD_PHASE_STAMPS
+                              , nullptr
+#endif
+                              );
+    if( valid ) a.out_prev[ gid ] = (int8_t)code;
+#ifdef FD_PHASE_STAMPS
+    if( args.stamps && (tid & 63) == 0 ) {           /* pipe stamps: [2] second phase cycles per wave, [7] its waves */
+      atomicAdd( &args.stamps[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - pt0) );
+      atomicAdd( &args.stamps[7], 1ull );
+    }
+#endif
+    return;
+  }
+
+  /* ---- first phase of the current batch ---- */
+  uint64_t nn = args.n;
+  if( (gid & ~(uint64_t)63) >= nn ) return;
+#ifdef FD_PHASE_STAMPS
+  uint64_t qt0 = __builtin_amdgcn_s_memtime();
+#endif
+  bool valid = gid < nn;
+  fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
+  if( valid ) d = args.desc[ gid ];
+  uint64_t asz = args.arena_sz;
+  bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
+                 (uint64_t)d.msg_off + d.msg_sz <= asz;
+  uint32_t lim_dw = (uint32_t)((asz + 3u) >> 2) + 1u;
+  uint32_t sig[ 16 ], pub[ 8 ];
+#pragma unroll
+  for( int j=0; j<16; j++ ) sig[j] = 0u;
+#pragma unroll
+  for( int j=0; j<8; j++ ) pub[j] = 0u;
+  if( desc_ok ) {
+    load_words<16>( sig, args.arena, d.sig_off, lim_dw );
+    load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
+  }
+  bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                           /* :157-159 */
+  bool live  = desc_ok && !bad_s;
+  uint8_t * grow = a.dig_cur + gid;
+  verify_prep_digits( grow, cap, tid, live, sig, pub, args, d, lim_dw
+#ifdef FD_PHASE_STAMPS
+                      , nullptr
+#endif
+                      );
+  FE_FENCE();
+#ifdef FD_PHASE_STAMPS
+  uint64_t qt1 = __builtin_amdgcn_s_memtime();
+#endif
+  int stA = 0;
+  if( live ) {
+    ge_p3 Q;
+    int ok = ge_decode( Q, pub, !args.ref_codes );
+    int sm = ge_affine_small_order( Q );
+    FE_FENCE();
+    if( ok && !sm ) vtab_build( args.vtab, args.vtab_cap, (2u*a.set_cur)*cap + gid, Q );
+    stA = (ok ? 1 : 0) | (sm ? 2 : 0);
+    FE_FENCE();
+  }
+#ifdef FD_PHASE_STAMPS
+  if( args.stamps && (tid & 63) == 0 ) {             /* pipe stamps: [0] SHA+lattice+digits, [1] decode+table of A */
+    uint64_t qt2 = __builtin_amdgcn_s_memtime();
+    atomicAdd( &args.stamps[0], (unsigned long long)(qt1 - qt0) );
+    atomicAdd( &args.stamps[1], (unsigned long long)(qt2 - qt1) );
+  }
+#endif
+  if( !valid ) return;
+  a.pcode_cur[ gid ] = (int8_t)(FD_PIPE_ST_VALID | (desc_ok ? FD_PIPE_ST_DESC : 0) | (bad_s ? FD_PIPE_ST_BADS : 0) |
+                                ((stA & 1) ? FD_PIPE_ST_A_OK : 0) | ((stA & 2) ? FD_PIPE_ST_A_SM : 0));
 }
 
 /* ------------------------------------------------------------------ SHA-512 batch */

@@ -68,6 +68,8 @@ def load_lib():
     lib.fd_ed25519_gpu_submit.argtypes = [vp, vp, u64, vp, u64, vp]
     lib.fd_ed25519_gpu_poll.argtypes = [vp]
     lib.fd_ed25519_verify_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_pipe_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_pipe_flush_dev.argtypes = [vp, i32, vp]
     lib.fd_ed25519_gpu_verify.argtypes = [vp, ctypes.c_char_p, u64, ctypes.c_char_p, ctypes.c_char_p,
                                           ctypes.POINTER(ctypes.c_int)]
     lib.fd_ed25519_gpu_verify_batch_single_msg.argtypes = [vp, ctypes.c_char_p, u64, ctypes.c_char_p,
@@ -220,6 +222,19 @@ class Ed25519Gpu:
                                                      d_out, stream)
         if r:
             raise GpuError("fd_ed25519_verify_batch_gpu_dev: %s (%d)" % (strerror(r), r))
+
+    def pipe_dev(self, d_arena, arena_sz, d_desc, desc_cnt, d_out, stream=0, dev_idx=0):
+        """Pipelined device-pointer entry (fd_ed25519_gpu_pipe_dev): enqueues this
+        batch's first phase beside the previous batch's second phase; the previous
+        batch's codes land in ITS d_out when this launch completes."""
+        r = self.lib.fd_ed25519_gpu_pipe_dev(self.ctx, dev_idx, d_arena, arena_sz, d_desc, desc_cnt, d_out, stream)
+        if r:
+            raise GpuError("fd_ed25519_gpu_pipe_dev: %s (%d)" % (strerror(r), r))
+
+    def pipe_flush_dev(self, stream=0, dev_idx=0):
+        r = self.lib.fd_ed25519_gpu_pipe_flush_dev(self.ctx, dev_idx, stream)
+        if r:
+            raise GpuError("fd_ed25519_gpu_pipe_flush_dev: %s (%d)" % (strerror(r), r))
 
     def verify(self, msg, sig, pub):
         """Mirror of fd_ed25519_verify: returns the FD_ED25519_* code."""

@@ -97,6 +97,55 @@ __global__ void __launch_bounds__(256, WPE) k_sqchain2(uint32_t* out, unsigned l
   if (a.v[0] == 0x12345678u) out[threadIdx.x] = a.v[1] + b.v[1];
 }
 
+/* the same doubling loop with only lanes 0..ACT-1 of each wave active (EXEC
+   upper bits clear for the whole loop): does a half-empty wave64 issue in
+   one 32-lane pass on gfx950's SIMD32? */
+template<int ACT>
+__global__ void __launch_bounds__(256, WPE) k_dbl_part(uint32_t* out, unsigned long long* cyc, int iters) {
+  if ((int)(threadIdx.x & 63) >= ACT) return;
+  ge_p3 p; INIT_P( p );
+  TIMED( ge_dbl( p, p, false ); ge_dbl( p, p, false ); ge_dbl( p, p, false ); ge_dbl( p, p, true ) )
+  if (p.X.v[0] == 0x12345678u) out[threadIdx.x] = p.Y.v[1] + p.T.v[2];
+}
+
+/* Co-running roles on one SIMD (the pipelined-kernel question): a block of
+   4*NW waves; waves 0-3 (one per SIMD) run the doubling loop (the chain) at
+   priority PRIO, waves 4.. run the squaring loop (the decode).  cyc[0] sums
+   the chain waves' cycles per dbl, cyc[1] the others' per sq. */
+template<int NW, int PRIO>
+__global__ void __launch_bounds__(256 * NW, 1) k_mix(uint32_t* out, unsigned long long* cyc, int iters) {
+  int w = threadIdx.x >> 6;
+  if (w < 4) {
+    if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+    ge_p3 p; INIT_P( p );
+    uint64_t t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+    for (int it = 0; it < iters; it++) { ge_dbl( p, p, false ); ge_dbl( p, p, false ); ge_dbl( p, p, false ); ge_dbl( p, p, true ); }
+    uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) atomicAdd(&cyc[0], (unsigned long long)(t1 - t0));
+    if (p.X.v[0] == 0x12345678u) out[threadIdx.x] = p.Y.v[1] + p.T.v[2];
+  } else {
+    fe a; for (int i = 0; i < 10; i++) a.v[i] = (threadIdx.x * 77u + i * 1313u) & 0x1ffffffu;
+    uint64_t t0 = __builtin_amdgcn_s_memtime();
+    int n = iters * 40;   /* about as long as the chain waves' loop alone */
+#pragma unroll 1
+    for (int it = 0; it < n; it++) { fe_sq( a, a ); }
+    uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) atomicAdd(&cyc[1], (unsigned long long)(t1 - t0));
+    if (a.v[0] == 0x12345678u) out[threadIdx.x] = a.v[1];
+  }
+}
+
+int run_mix(const char* name, void (*f)(uint32_t*, unsigned long long*, int), int nw, int iters) {
+  uint32_t* d; unsigned long long* c; CHECK(hipMalloc(&d, 1 << 16)); CHECK(hipMalloc(&c, 16));
+  for (int rep = 0; rep < 2; rep++) { CHECK(hipMemset(c, 0, 16)); hipLaunchKernelGGL(f, dim3(256), dim3(256 * nw), 0, 0, d, c, iters); CHECK(hipDeviceSynchronize()); }
+  unsigned long long h[2]; CHECK(hipMemcpy(h, c, 16, hipMemcpyDeviceToHost));
+  double dbl = (double)h[0] / (256 * 4.0) / (iters * 4.0);
+  double sq = nw > 1 ? (double)h[1] / (256 * 4.0 * (nw - 1)) / (iters * 40.0) : 0.0;
+  printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"chain_cyc_per_dbl\": %.1f, \"other_cyc_per_sq\": %.1f}\n", name, nw, dbl, sq);
+  CHECK(hipFree(d)); CHECK(hipFree(c)); return 0;
+}
+
 typedef void (*kfn)(uint32_t*, unsigned long long*, int);
 int run(const char* name, kfn f, int iters, double per) {
   uint32_t* d; unsigned long long* c; CHECK(hipMalloc(&d, 4096)); CHECK(hipMalloc(&c, 8));
@@ -106,9 +155,20 @@ int run(const char* name, kfn f, int iters, double per) {
   printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"cyc_per_op_per_wave\": %.1f}\n", name, WPE, (double)h / (blocks * 4.0) / (iters * per));
   CHECK(hipFree(d)); CHECK(hipFree(c)); return 0;
 }
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) {
+    run_mix("chain alone", k_mix<1, 0>, 1, 100);
+    run_mix("chain + 1 sq wave, prio 0", k_mix<2, 0>, 2, 100);
+    run_mix("chain + 1 sq wave, chain prio 3", k_mix<2, 3>, 2, 100);
+    run_mix("chain + 2 sq waves, chain prio 3", k_mix<3, 3>, 3, 100);
+    run_mix("chain + 3 sq waves, chain prio 3", k_mix<4, 3>, 4, 100);
+    run_mix("chain + 3 sq waves, prio 0", k_mix<4, 0>, 4, 100);
+    return 0;
+  }
   run("ge_dbl x4 (3 no-T + 1 T), per dbl", k_dbl, 200, 4.0);
   run("ge_dbl interleaved, per dbl", k_dbl_il, 200, 4.0);
+  run("ge_dbl, 32 of 64 lanes active, per dbl", k_dbl_part<32>, 200, 4.0);
+  run("ge_dbl, 16 of 64 lanes active, per dbl", k_dbl_part<16>, 200, 4.0);
   run("ge_add_cached (T + no-T), per add", k_add, 400, 2.0);
   run("ge_add_cached interleaved, per add", k_add_il, 400, 2.0);
   run("fe_sq chains a,b alone, per sq", k_sqchain, 1000, 4.0);
