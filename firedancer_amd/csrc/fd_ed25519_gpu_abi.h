@@ -65,30 +65,49 @@ struct verify_args {
   uint64_t                  kcap;      /* slots */
 };
 
-/* Pipelined verify (fd_ed25519_verify_pipe_kernel): one launch runs the
-   first phase (checks, SHA-512, lattice, digits, decode and table of A) of
-   batch "cur" beside the second phase (decode and table of R, the final
-   check-order code, the scalar multiplication and compare) of the previous
-   batch "prev", whose first phase ran in the previous launch.  Between the
-   two phases a batch lives in HBM: its tables in set s of the pipe table
-   scratch (A of slot g at table 2 s sig_cap + g, R at (2 s + 1) sig_cap + g;
-   v.vtab_cap = 4 sig_cap), its digit rows (FD_ROWS rows of sig_cap bytes,
-   the LDS row layout) and its partial status per slot (FD_PIPE_ST_* bits,
-   fd_ed25519_gpu_kern.hip); the previous batch's arena and descriptors are
-   read again for R. */
+/* Pipelined verify (fd_ed25519_verify_pipe_kernel): one launch runs phase
+   A (checks, SHA-512, lattice, w, decode and table of A) of batch j, phase B
+   (decode and table of R, the check-order code, the top kb windows of the
+   chain) of batch j-1 and phase C (the other windows, [w]B, the compare) of
+   batch j-2.  Between launches a batch lives in HBM, in the set its phase A
+   was given (3 sets, batches in flight take different ones):
+     tables: A of slot g at table (2 s) sig_cap + g, R at (2 s + 1) sig_cap + g
+       of v.vtab (v.vtab_cap = 6 sig_cap);
+     hand-off words [FD_PH_WORDS][sig_cap] (R's encoding, the biased digit
+       scalars), a status byte per slot (FD_PIPE_ST_* bits,
+       fd_ed25519_gpu_kern.hip), the window count per 64-slot wave;
+   and from phase B to phase C (2 sets): the partial sum [FD_PACC_WORDS][sig_cap]
+   and the code of the checks per slot.  The arena and descriptors are read by
+   phase A only. */
+#define FD_PH_R           0            /* R's encoding, 8 words                        */
+#define FD_PH_YU          8            /* u + 8 (16^0 + ... + 16^(nw-2)), 8 words      */
+#define FD_PH_YV          16           /* v + the same bias, 8 words                   */
+#define FD_PH_YW          24           /* w + 2^15 (2^0 + ... + 2^224), 8 words        */
+#define FD_PH_WORDS       32
+#define FD_PACC_WORDS     40           /* X, Y, Z, T                                   */
+#define FD_PIPE_SETS      3
 struct pipe_args {
-  verify_args               v;          /* arena, arena_sz, desc, n (= cur count), ctab, vtab, vtab_cap, ref_codes */
-  uint64_t                  sig_cap;    /* slots per table set / digit rows */
-  uint64_t                  set_cur;    /* 0 / 1: cur writes set_cur, prev is read from set_cur ^ 1 */
-  uint8_t *                 dig_cur;    /* FD_ROWS x sig_cap */
-  int8_t *                  pcode_cur;  /* sig_cap */
-  uint8_t const *           dig_prev;
-  int8_t const *            pcode_prev;
-  uint64_t                  n_prev;     /* 0: no previous batch */
-  int8_t *                  out_prev;   /* codes of the previous batch */
-  uint8_t const *           arena_prev; /* the previous batch's arena and descriptors (R is decoded from them) */
-  uint64_t                  arena_sz_prev;
-  fd_ed25519_desc_t const * desc_prev;
+  verify_args               v;          /* phase A's arena, arena_sz, desc, n; ctab, vtab, vtab_cap, ref_codes, stamps */
+  uint64_t                  sig_cap;    /* slots per set */
+  uint64_t                  kb;         /* windows of the chain in phase B (>= 1) */
+  uint64_t                  prio;       /* wave priority of phase C / B / A: bits 0-1 / 2-3 / 4-5 */
+  uint64_t                  set_a, set_b, set_c;
+  uint32_t *                hand_a;     /* phase A writes */
+  uint8_t *                 st_a;
+  uint8_t *                 nw_a;
+  uint32_t const *          hand_b;     /* phase B reads */
+  uint8_t const *           st_b;
+  uint8_t const *           nw_b;
+  uint64_t                  n_b;        /* 0: no batch in phase B */
+  uint32_t *                acc_b;      /* phase B writes */
+  int8_t *                  code_b;
+  uint32_t const *          hand_c;     /* phase C reads */
+  uint8_t const *           st_c;
+  uint8_t const *           nw_c;
+  uint32_t const *          acc_c;
+  int8_t const *            code_c;
+  uint64_t                  n_c;        /* 0: no batch in phase C */
+  int8_t *                  out_c;      /* the codes of batch j-2 */
 };
 
 struct kpart_args {

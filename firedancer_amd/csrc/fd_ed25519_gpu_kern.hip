@@ -352,11 +352,47 @@ __device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 
   }
 }
 
-/* k = SHA-512(R||A||M) mod l, the lattice vector (u, v), w = v S mod l, and
-   their digits into this lane's column drow (rows FD_ROW_U / _V / _W, row r
-   at drow[r * stride]: LDS with stride FD_VERIFY_BLOCK, or the pipelined
-   kernel's HBM rows; FD_ROW_NW: the wave-uniform window count, written by
-   lane 0 of each wave).  Lanes that are not live write zero digits (every
+/* k = SHA-512(R||A||M) mod l (:203-206), the lattice vector (u, v, sign
+   of u) of k (fd_lattice_dev.h) and w = v S mod l, for a live lane; *nbits =
+   the longer of u, v in bits. */
+__device__ __forceinline__ void verify_prep_scalars( uint32_t u[ 8 ], uint32_t v[ 8 ], int * un, uint32_t w[ 8 ], int * nbits,
+                                                     uint32_t const sig[ 16 ], uint32_t const pub[ 8 ], verify_args const & args,
+                                                     fd_ed25519_desc_t const & d, uint32_t lim_dw
+#ifdef FD_PHASE_STAMPS
+                                                     , uint64_t * _st
+#endif
+                                                     ) {
+  uint32_t k[ 8 ];
+  hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );
+  FE_FENCE();
+  STAMP( 2 );
+  lat_short_vector( k, u, v, un );
+  FE_FENCE();
+  uint32_t pr[ 16 ];                                                 /* w = v S mod l */
+#pragma unroll
+  for( int j=0; j<16; j++ ) pr[j] = 0u;
+#pragma unroll
+  for( int i=0; i<8; i++ ) {
+    uint64_t c = 0;
+#pragma unroll
+    for( int j=0; j<8; j++ ) { uint64_t t = (uint64_t)v[i] * sig[8+j] + pr[i+j] + c; pr[i+j] = (uint32_t)t; c = t >> 32; }
+    pr[i+8] = (uint32_t)c;
+  }
+  sc_reduce512( w, pr );
+  *nbits = max( bitlen8( u ), bitlen8( v ) );
+}
+
+/* The wave-uniform window count: x < 2^(4 nw - 1) for every lane's u, v. */
+__device__ __forceinline__ int wave_windows( int nbits ) {
+#pragma unroll
+  for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
+  return min( FD_NDIG_MAX, max( 32, (nbits + 4) >> 2 ) );
+}
+
+/* k, the lattice vector, w = v S mod l and their digits into this lane's
+   column drow (rows FD_ROW_U / _V / _W, row r at drow[r * stride], LDS with
+   stride FD_VERIFY_BLOCK; FD_ROW_NW: the wave-uniform window count, written
+   by lane 0 of each wave).  Lanes that are not live write zero digits (every
    lane takes part in the wave max). */
 __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, uint64_t stride, int tid, bool live, uint32_t const sig[ 16 ],
                                                     uint32_t const pub[ 8 ], verify_args const & args,
@@ -370,24 +406,12 @@ __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, uint64_t str
 #pragma unroll
   for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; }
   if( live ) {
-    uint32_t k[ 8 ];
-    hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );  /* :203-206 */
-    FE_FENCE();
-    STAMP( 2 );
-    lat_short_vector( k, u, v, &un );
-    FE_FENCE();
-    uint32_t pr[ 16 ];                                                 /* w = v S mod l */
-#pragma unroll
-    for( int j=0; j<16; j++ ) pr[j] = 0u;
-#pragma unroll
-    for( int i=0; i<8; i++ ) {
-      uint64_t c = 0;
-#pragma unroll
-      for( int j=0; j<8; j++ ) { uint64_t t = (uint64_t)v[i] * sig[8+j] + pr[i+j] + c; pr[i+j] = (uint32_t)t; c = t >> 32; }
-      pr[i+8] = (uint32_t)c;
-    }
     uint32_t w[ 8 ];
-    sc_reduce512( w, pr );
+    verify_prep_scalars( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
+#ifdef FD_PHASE_STAMPS
+                         , _st
+#endif
+                         );
     /* signed 16-bit windows: d_k in [-2^15, 2^15), the top one (w < 2^253)
        keeps its carry: d_15 <= 2^13 */
     int c = 0;
@@ -399,16 +423,12 @@ __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, uint64_t str
       drow[ (uint64_t)(FD_ROW_W + 2*k    )*stride ] = (uint8_t)(dd & 255);
       drow[ (uint64_t)(FD_ROW_W + 2*k + 1)*stride ] = (uint8_t)((dd >> 8) & 255);
     }
-    nbits = max( bitlen8( u ), bitlen8( v ) );
   }
-  /* wave-uniform window count: x < 2^(4 nw - 1) for every lane's u, v */
-#pragma unroll
-  for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
-  int nw = min( FD_NDIG_MAX, max( 32, (nbits + 4) >> 2 ) );
+  int nw = wave_windows( nbits );
   recode4_lds( drow + FD_ROW_U*stride, u, un, nw, stride );
   recode4_lds( drow + FD_ROW_V*stride, v, 0,  nw, stride );
   if( (tid & 63) == 0 ) drow[ FD_ROW_NW*stride ] = (uint8_t)nw;
-  }
+}
 
 /* The verify code from the check results, in the reference's order
    (fd_ed25519_user.c:157-228): 0 means every check before the equation
@@ -478,6 +498,146 @@ __device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_
   return code;
 }
 
+/* ------------------------------------------------------------------ LDS-DMA chain */
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+/* One table entry (10 x 16 B per lane) into the wave's LDS buffer
+   buf[10][64] by LDS-DMA. */
+__device__ __forceinline__ void vtab_fetch_lds( uint4 * buf, uint32_t const * vtab, uint64_t cap, uint64_t t, uint32_t db ) {
+  uint32_t e = min( db < 8u ? 8u - db : db - 8u, 8u );
+  uint4 const * m; uint4 const * tl;
+  vtab_ptrs( vtab, cap, t, e, &m, &tl );
+#pragma unroll
+  for( int j=0; j<8; j++ ) __builtin_amdgcn_global_load_lds( (void const *)(m + j), (lds_void_t *)(buf + 64*j), 16, 0, 0 );
+#pragma unroll
+  for( int j=0; j<2; j++ ) __builtin_amdgcn_global_load_lds( (void const *)(tl + j), (lds_void_t *)(buf + 64*(8+j)), 16, 0, 0 );
+}
+
+/* Comb-table entry |d| of position k into buf[8][64]. */
+__device__ __forceinline__ void ctab_fetch_lds( uint4 * buf, uint32_t const * ctab, int k, int d ) {
+  uint32_t e = (uint32_t)(d < 0 ? -d : d);
+  uint4 const * p = (uint4 const *)(ctab + ((uint64_t)k * FD_CTAB_N + e) * FD_CTAB_STRIDE);
+#pragma unroll
+  for( int j=0; j<8; j++ ) __builtin_amdgcn_global_load_lds( (void const *)(p + j), (lds_void_t *)(buf + 64*j), 16, 0, 0 );
+}
+
+/* The wave's LDS-DMA has landed (this wave's only vector-memory operations
+   in flight are its own table fetches). */
+__device__ __forceinline__ void dma_wait( void ) {
+  FE_FENCE();
+  __builtin_amdgcn_s_waitcnt( 0x0f70 );      /* vmcnt(0) */
+  FE_FENCE();
+}
+
+template<int N>
+__device__ __forceinline__ void lds_words( uint32_t w[ 4*N ], uint4 const * buf, int lane ) {
+#pragma unroll
+  for( int j=0; j<N; j++ ) { uint4 v = buf[ 64*j + lane ]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
+}
+
+/* Biased 4-bit digit i (0..16) of a recoded scalar y = x + 8 (16^0 + ... +
+   16^(nw-2)) held in the wave's LDS column block y[8][64]: nibble i is
+   d_i + 8 below the top window and d_i at the top one (recode4_lds's
+   digits, read off the bits), negated when neg. */
+__device__ __forceinline__ uint32_t ydig( uint32_t const * y, int lane, int i, int nw, bool neg ) {
+  uint32_t db = ((y[ (i >> 3)*64 + lane ] >> (4*(i & 7))) & 15u) + (i == nw-1 ? 8u : 0u);
+  return neg ? 16u - db : db;
+}
+
+/* x + 8 (16^0 + ... + 16^(nw-2)): the signed 4-bit recoding of x < 2^(4 nw - 1)
+   as a bias (digit i = nibble i - 8, the top one unbiased: recode4_lds). */
+__device__ __forceinline__ void ybias4( uint32_t y[ 8 ], uint32_t const x[ 8 ], int nw ) {
+  uint64_t c = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) {
+    int nb = nw - 1 - 8*j;                          /* biased nibbles in word j */
+    uint32_t pat = nb >= 8 ? 0x88888888u : (nb <= 0 ? 0u : (0x88888888u & ((1u << (4*nb)) - 1u)));
+    c += (uint64_t)x[j] + pat;
+    y[j] = (uint32_t)c; c >>= 32;
+  }
+}
+
+/* w + 2^15 (2^0 + 2^16 + ... + 2^224): the signed 16-bit comb digits as a
+   bias (digit k = half k - 2^15 for k < 15, the top one unbiased). */
+__device__ __forceinline__ void ybias16( uint32_t y[ 8 ], uint32_t const w[ 8 ] ) {
+  uint64_t c = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) { c += (uint64_t)w[j] + (j < 7 ? 0x80008000u : 0x00008000u); y[j] = (uint32_t)c; c >>= 32; }
+}
+
+/* Windows hi-1 .. lo of the Straus chain acc = [u](-A) + [v](-R) (dsm_loop's
+   order: four doublings unless it is the chain's first window, then A's and
+   R's entries); entries staged in buf one addition ahead; T computed at the
+   last window of the segment (the next phase starts with a doubling or the
+   comb). */
+__device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t const * yu, uint32_t const * yv, int lane,
+                                           bool uneg, uint32_t const * vtab, uint64_t cap, uint64_t ta, uint64_t tr,
+                                           int nw, int hi, int lo ) {
+  uint32_t dba = ydig( yu, lane, hi-1, nw, uneg );
+  vtab_fetch_lds( buf, vtab, cap, ta, dba );
+#pragma unroll 1
+  for( int i=hi-1; i>=lo; i-- ) {
+    if( i < nw-1 ) {
+#pragma unroll 1
+      for( int j=0; j<3; j++ ) { ge_dbl( acc, acc, false ); FE_FENCE(); }
+      ge_dbl( acc, acc, true );
+      FE_FENCE();
+    }
+    ge_cached q;
+    uint32_t dbr;
+    {
+      dma_wait();
+      uint32_t w[ 40 ];
+      lds_words<10>( w, buf, lane );
+      dbr = ydig( yv, lane, i, nw, false );
+      FE_FENCE();
+      vtab_fetch_lds( buf, vtab, cap, tr, dbr );     /* LDS reads issued before the DMA see the old bytes */
+      vtab_finish( q, w, dba );
+    }
+    FE_FENCE();
+    ge_add_cached( acc, acc, q, true );
+    FE_FENCE();
+    {
+      dma_wait();
+      uint32_t w[ 40 ];
+      lds_words<10>( w, buf, lane );
+      if( i > lo ) dba = ydig( yu, lane, i-1, nw, uneg );
+      FE_FENCE();
+      if( i > lo ) vtab_fetch_lds( buf, vtab, cap, ta, dba );
+      vtab_finish( q, w, dbr );
+    }
+    FE_FENCE();
+    ge_add_cached( acc, acc, q, i == lo );
+    FE_FENCE();
+  }
+}
+
+/* acc += [w]B: the 16 comb-table additions, w's biased digits in yw. */
+__device__ __forceinline__ void comb_lds( ge_p3 & acc, uint4 * buf, uint32_t const * yw, int lane, uint32_t const * ctab ) {
+#define FD_WDIG( k ) ((int)((yw[ ((k) >> 1)*64 + lane ] >> (16*((k) & 1))) & 0xffffu) - ((k) < FD_CTAB_POS-1 ? 32768 : 0))
+  int d = FD_WDIG( 0 );
+  ctab_fetch_lds( buf, ctab, 0, d );
+#pragma unroll 1
+  for( int k=0; k<FD_CTAB_POS; k++ ) {
+    ge_precomp bp;
+    {
+      dma_wait();
+      uint32_t w[ 32 ];
+      lds_words<8>( w, buf, lane );
+      int dn = k + 1 < FD_CTAB_POS ? FD_WDIG( k + 1 ) : 0;
+      FE_FENCE();
+      if( k + 1 < FD_CTAB_POS ) ctab_fetch_lds( buf, ctab, k + 1, dn );
+      ctab_finish( bp, w, d );
+      d = dn;
+    }
+    FE_FENCE();
+    ge_madd( acc, acc, bp, k + 1 < FD_CTAB_POS );
+    FE_FENCE();
+  }
+#undef FD_WDIG
+}
+
 /* One signature per lane:
      S check -> k = SHA-512(R||A||M) mod l -> (u, v) short vector of k mod 8l,
      w = v S mod l, digits -> LDS -> decode A and R, small-order checks,
@@ -487,9 +647,11 @@ __device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_
    decode R, small-order A, small-order R, equation. */
 extern "C" __global__ void __launch_bounds__( FD_VERIFY_BLOCK, FD_VERIFY_WAVES_PER_EU )
 fd_ed25519_verify_kernel( verify_args args ) {
-  __shared__ uint8_t  s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
+  __shared__ uint4    s_buf[ 4 ][ 10*64 ];     /* a table / comb entry per wave (LDS-DMA) */
+  __shared__ uint32_t s_y[ 4 ][ 24*64 ];       /* per wave: biased u, v, w (8 words each) */
 
   int tid = (int)threadIdx.x;
+  int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane( tid >> 6 );
 #ifdef FD_PHASE_STAMPS
   uint64_t _st[ FD_NSTAMP ] = { 0, 0, 0, 0, 0, 0, 0, 0 };
 #endif
@@ -526,24 +688,49 @@ fd_ed25519_verify_kernel( verify_args args ) {
   bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                           /* :157-159 */
   bool live  = desc_ok && !bad_s;
 
-  /* k, lattice vector, w and digits (before the decodes: only digits stay live) */
-  uint8_t * drow = s_dig + tid;
-  verify_prep_digits( drow, FD_VERIFY_BLOCK, tid, live, sig, pub, args, d, lim_dw
+  /* k, the lattice vector (u, v), w; their biased digits into this lane's
+     LDS column (before the decodes: only they and the sign of u stay live) */
+  uint32_t * y = s_y[ wv ];
+  int un = 0, nwin = 32;
+  {
+    uint32_t u[ 8 ], v[ 8 ], w[ 8 ];
+    int nbits = 0;
+#pragma unroll
+    for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; w[j] = 0u; }
+    if( live ) verify_prep_scalars( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
 #ifdef FD_PHASE_STAMPS
-                      , _st
+                                    , _st
 #endif
-                      );
+                                    );
+    int nw = wave_windows( nbits );
+    uint32_t t[ 8 ];
+    ybias4( t, u, nw );
+#pragma unroll
+    for( int j=0; j<8; j++ ) y[ j*64 + lane ] = t[j];
+    ybias4( t, v, nw );
+#pragma unroll
+    for( int j=0; j<8; j++ ) y[ (8 + j)*64 + lane ] = t[j];
+    ybias16( t, w );
+#pragma unroll
+    for( int j=0; j<8; j++ ) y[ (16 + j)*64 + lane ] = t[j];
+    nwin = nw;
+  }
   FE_FENCE();
 
-  /* decode A then R (:162 frombytes_2x), small order (:193-198), tables */
+  /* decode A then R (:162 frombytes_2x), small order (:193-198), tables;
+     the two encodings wait in the wave's (still idle) LDS-DMA buffer, so
+     they hold no registers across the decodes */
   STAMP( 3 );
+  uint32_t * encs = (uint32_t *)s_buf[ wv ];
+#pragma unroll
+  for( int j=0; j<8; j++ ) { encs[ j*64 + lane ] = pub[j]; encs[ (8 + j)*64 + lane ] = sig[j]; }
   int st[ 2 ] = { 0, 0 };
   if( live ) {
 #pragma unroll 1
     for( int q=0; q<2; q++ ) {
       uint32_t enc[ 8 ];
 #pragma unroll
-      for( int j=0; j<8; j++ ) enc[j] = q ? sig[j] : pub[j];
+      for( int j=0; j<8; j++ ) enc[j] = encs[ (8*q + j)*64 + lane ];
       ge_p3 Q;
       int ok = ge_decode( Q, enc, !args.ref_codes );
       int sm = ge_affine_small_order( Q );
@@ -558,16 +745,25 @@ fd_ed25519_verify_kernel( verify_args args ) {
   STAMP( 4 );
 
   if( !valid ) return;
-  int code = verify_tail( args, desc_ok, bad_s, stA, stR, drow, s_dig, tid, gid, nullptr
-#ifdef FD_PHASE_STAMPS
-                          , _st
-#endif
-                          );
+  int code = verify_precode( args, desc_ok, bad_s, stA, stR );
+  if( code == 0 ) {
+    /* Q = [u](-A) + [v](-R) + [w]B, Q == O  (:225-228 on [v]D) */
+    int nw = __builtin_amdgcn_readfirstlane( nwin );
+    ge_p3 acc; ge_identity( acc );
+    chain_seg( acc, s_buf[ wv ], y, y + 8*64, lane, un != 0, args.vtab, cap, gid, cap/2u + gid, nw, nw, 0 );
+    comb_lds( acc, s_buf[ wv ], y + 16*64, lane, args.ctab );
+    STAMP( 5 );
+    fe dl;
+    int ex = fe_is_zero( acc.X );
+    fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
+    int ey = fe_is_zero( dl );
+    code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  }
   args.out[ di ] = (int8_t)code;
 #ifdef FD_PHASE_STAMPS
   STAMP( 6 );
   if( args.stamps && (tid & 63) == 0 ) {
-    /* 0-1 prologue+table copy, 1-2 SHA (live lanes), 2-3 lattice+digits, 3-4 decodes+tables, 4-5 loop, 5-6 tail */
+    /* 0-1 prologue, 1-2 SHA (live lanes), 2-3 lattice+digits, 3-4 decodes+tables, 4-5 chain+comb, 5-6 compare */
     for( int i=0; i<6; i++ ) atomicAdd( &args.stamps[i], (unsigned long long)(_st[i+1] - _st[i]) );
     atomicAdd( &args.stamps[7], 1ull );
   }
@@ -677,156 +873,212 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
   args.out[ gid ] = (int8_t)code;
 }
 
-/* Pipelined form (throughput): one launch runs the first phase of batch
-   "cur" and the second phase of the batch before it, in the two halves of
-   512-thread workgroups that share nothing (different batches: a batch's
-   A tables, digits and partial status cross the launch boundary in HBM,
-   pipe_args), so there is no barrier:
-     waves 0-3 (role 0, priority 3), previous batch: decode R, small-order R,
-       R's table, the final check-order code, then for lanes still passing
-       the Straus chain + [w]B + the compare;
-     waves 4-7 (role 1), current batch: descriptor / S checks, SHA-512,
-       lattice, digits, decode A, small-order A, A's table.
-   Why: one 64-signature wave per SIMD leaves VALU issue slots empty during
-   the chain; a second wave of independent work fills them without slowing
-   the first (tools/fe_probe2.hip mix probe: a doubling wave at priority 3
-   keeps its 3,854 cycles per doubling beside 1-3 squaring waves, which get
-   0.1-0.2 instructions per cycle).  The split balances the two: role 0 runs
-   at ~0.24 VALU instructions per cycle, role 1 on the leftover ~0.08, so
-   role 0 takes the larger share (R's decode and table, ~31 K instructions,
-   moved over: the first version with both decodes in role 1 left role 1 at
-   1.35 M cycles per wave against role 0's 1.05 M).  Same device functions
-   and check order as fd_ed25519_verify_kernel: bit-identical codes. */
-#define FD_PIPE_ST_VALID  0x80      /* partial status of the first phase (pcode byte) */
-#define FD_PIPE_ST_DESC   0x01      /* descriptor inside the arena   */
-#define FD_PIPE_ST_BADS   0x02      /* S >= l                        */
-#define FD_PIPE_ST_A_OK   0x04      /* A decodes                     */
-#define FD_PIPE_ST_A_SM   0x08      /* A has small order             */
-extern "C" __global__ void __launch_bounds__( 2 * FD_VERIFY_BLOCK, 1 )
+/* Pipelined form (throughput): one launch runs three phases of three
+   consecutive batches side by side, in the three 256-thread thirds of
+   768-thread workgroups (waves i, i+4, i+8 share SIMD i: three waves per
+   SIMD, none of them idle):
+     waves 8-11 (phase A), batch j:   descriptor / S checks, SHA-512, lattice
+       vector (u, v), w = v S mod l, decode A, small-order A, A's table;
+     waves 4-7  (phase B), batch j-1: decode R, small-order R, R's table, the
+       check-order code, then the TOP kb windows of the Straus chain;
+     waves 0-3  (phase C), batch j-2: the remaining windows, the 16 comb
+       additions of [w]B and the compare.
+   Why: config 2 is one 64-signature wave per SIMD, and one wave issues at
+   most one VALU instruction per ~4.4 cycles while the SIMD takes more from
+   other waves (tools/fe_probe2.hip: 1.40x the doubling throughput at two
+   waves, 1.75x at four).  Splitting the work of a signature over three
+   launches gives every SIMD three independent waves of similar length.
+   A batch crosses the launches in HBM: phase A leaves R's encoding, the
+   digit scalars (u, v, w plus their recoding bias, so each consumer reads
+   its signed digits straight off the bits) and a status byte per slot and
+   the window count per wave; phase B leaves the partial sum (X, Y, Z, T)
+   and the code of the checks.  The chain phases stage their table entries
+   in LDS by LDS-DMA (global_load_lds_dwordx4), one entry ahead, instead
+   of in 40 VGPRs: 168 VGPRs are the budget of three waves per SIMD.  Same
+   device functions and check order as fd_ed25519_verify_kernel:
+   bit-identical codes. */
+#define FD_PIPE_ST_VALID  0x80      /* phase A status byte                    */
+#define FD_PIPE_ST_DESC   0x01      /* descriptor inside the arena            */
+#define FD_PIPE_ST_BADS   0x02      /* S >= l                                 */
+#define FD_PIPE_ST_A_OK   0x04      /* A decodes                              */
+#define FD_PIPE_ST_A_SM   0x08      /* A has small order                      */
+#define FD_PIPE_ST_UNEG   0x10      /* the lattice u is negated               */
+
+/* The wave's digit scalars (words [w0, w0 + nwords) of the hand-off, row
+   stride cap) into its LDS column block y[nwords][64]. */
+__device__ __forceinline__ void hand_to_lds( uint32_t * y, uint32_t const * hand, uint64_t cap, uint64_t gid, int lane,
+                                             int w0, int nwords ) {
+#pragma unroll 1
+  for( int j=0; j<nwords; j++ ) y[ j*64 + lane ] = hand[ (uint64_t)(w0 + j)*cap + gid ];
+}
+
+extern "C" __global__ void __launch_bounds__( 3 * FD_VERIFY_BLOCK, 1 )
 fd_ed25519_verify_pipe_kernel( pipe_args a ) {
-  __shared__ uint8_t s_dig[ FD_ROWS * FD_VERIFY_BLOCK ];
-  int role = (int)threadIdx.x >> 8;                  /* wave-uniform */
+  __shared__ uint4    s_buf[ 2 ][ 4 ][ 10*64 ];       /* phase C / B: a table entry per wave      */
+  __shared__ uint32_t s_y[ 2 ][ 4 ][ 24*64 ];         /* phase C / B: u, v, w digit scalars       */
+  int role = __builtin_amdgcn_readfirstlane( (int)threadIdx.x >> 8 );   /* 0: phase C, 1: phase B, 2: phase A */
   int tid  = (int)threadIdx.x & (FD_VERIFY_BLOCK - 1);
+  int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane( tid >> 6 );
   uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)tid;
   uint64_t cap = a.sig_cap;
   verify_args const & args = a.v;
-
-  if( role == 0 ) {
-    /* ---- second phase of the previous batch ---- */
-    uint64_t np = a.n_prev;
-    if( (gid & ~(uint64_t)63) >= np ) return;        /* whole waves past it */
-    __builtin_amdgcn_s_setprio( 3 );
+  uint64_t vcap = args.vtab_cap;
+  switch( (int)(a.prio >> (2*role)) & 3 ) {            /* wave priority (age decides among equals) */
+    case 1:  __builtin_amdgcn_s_setprio( 1 ); break;
+    case 2:  __builtin_amdgcn_s_setprio( 2 ); break;
+    case 3:  __builtin_amdgcn_s_setprio( 3 ); break;
+    default: break;
+  }
 #ifdef FD_PHASE_STAMPS
-    uint64_t pt0 = __builtin_amdgcn_s_memtime();
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-    bool valid = gid < np;
-    int ps = valid ? (int)(uint8_t)a.pcode_prev[ gid ] : 0;
-    bool desc_ok = (ps & FD_PIPE_ST_DESC) != 0, bad_s = (ps & FD_PIPE_ST_BADS) != 0;
-    int stA = ((ps & FD_PIPE_ST_A_OK) ? 1 : 0) | ((ps & FD_PIPE_ST_A_SM) ? 2 : 0);
-    uint64_t sp = a.set_cur ^ 1u;
-    /* R = sig[0:32] of the previous batch: decode, small order, table */
-    int stR = 0;
-    if( desc_ok && !bad_s ) {
-      fd_ed25519_desc_t d = a.desc_prev[ gid ];
-      uint32_t lim_dw = (uint32_t)((a.arena_sz_prev + 3u) >> 2) + 1u;
-      uint32_t enc[ 8 ];
-      load_words<8>( enc, a.arena_prev, d.sig_off, lim_dw );
+
+  if( role == 2 ) {
+    /* ---- phase A, batch j ---- */
+    uint64_t nn = args.n;
+    if( (gid & ~(uint64_t)63) >= nn ) return;
+    bool valid = gid < nn;
+    fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
+    if( valid ) d = args.desc[ gid ];
+    uint64_t asz = args.arena_sz;
+    bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
+                   (uint64_t)d.msg_off + d.msg_sz <= asz;
+    uint32_t lim_dw = (uint32_t)((asz + 3u) >> 2) + 1u;
+    uint32_t sig[ 16 ], pub[ 8 ];
+#pragma unroll
+    for( int j=0; j<16; j++ ) sig[j] = 0u;
+#pragma unroll
+    for( int j=0; j<8; j++ ) pub[j] = 0u;
+    if( desc_ok ) {
+      load_words<16>( sig, args.arena, d.sig_off, lim_dw );
+      load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
+    }
+    bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                         /* :157-159 */
+    bool live  = desc_ok && !bad_s;
+    uint32_t u[ 8 ], v[ 8 ], w[ 8 ];
+    int un = 0, nbits = 0;
+#pragma unroll
+    for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; w[j] = 0u; }
+    if( live ) verify_prep_scalars( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
+#ifdef FD_PHASE_STAMPS
+                                    , nullptr
+#endif
+                                    );
+    FE_FENCE();
+    int nw = wave_windows( nbits );
+    if( valid ) {
+      uint32_t * h = a.hand_a + gid;
+      uint32_t y[ 8 ];
+#pragma unroll
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_R + j)*cap ] = sig[j];
+      ybias4( y, u, nw );
+#pragma unroll
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YU + j)*cap ] = y[j];
+      ybias4( y, v, nw );
+#pragma unroll
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YV + j)*cap ] = y[j];
+      ybias16( y, w );
+#pragma unroll
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YW + j)*cap ] = y[j];
+    }
+    if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)nw;
+    FE_FENCE();
+    int stA = 0;
+    if( live ) {
       ge_p3 Q;
-      int ok = ge_decode( Q, enc, !args.ref_codes );
+      int ok = ge_decode( Q, pub, !args.ref_codes );
       int sm = ge_affine_small_order( Q );
       FE_FENCE();
-      if( ok && !sm && (stA & 1) && !(stA & 2) ) vtab_build( args.vtab, args.vtab_cap, (2u*sp + 1u)*cap + gid, Q );
-      stR = (ok ? 1 : 0) | (sm ? 2 : 0);
+      if( ok && !sm ) vtab_build( args.vtab, vcap, (2u*a.set_a)*cap + gid, Q );
+      stA = (ok ? 1 : 0) | (sm ? 2 : 0);
       FE_FENCE();
     }
-    int code = verify_precode( args, desc_ok, bad_s, stA, stR );
-    /* this lane's digit column from the HBM rows into its LDS column */
-    uint8_t * drow = s_dig + tid;
-    uint8_t const * g = a.dig_prev + gid;
-    int nw = (int)g[ (uint64_t)FD_ROW_NW * cap - (uint64_t)(tid & 63) ];   /* lane 0 of the wave wrote it */
-    nw = __builtin_amdgcn_readfirstlane( nw );
-    if( (tid & 63) == 0 ) drow[ FD_ROW_NW*FD_VERIFY_BLOCK ] = (uint8_t)nw;
-    bool run = valid && code == 0;
-    if( run ) {
-#pragma unroll 4
-      for( int i=0; i<nw; i++ ) {
-        drow[ (FD_ROW_U + i)*FD_VERIFY_BLOCK ] = g[ (uint64_t)(FD_ROW_U + i) * cap ];
-        drow[ (FD_ROW_V + i)*FD_VERIFY_BLOCK ] = g[ (uint64_t)(FD_ROW_V + i) * cap ];
-      }
-#pragma unroll 8
-      for( int i=0; i<2*FD_CTAB_POS; i++ ) drow[ (FD_ROW_W + i)*FD_VERIFY_BLOCK ] = g[ (uint64_t)(FD_ROW_W + i) * cap ];
-    }
-    __builtin_amdgcn_wave_barrier();
-    if( run )
-      code = verify_equation( args, drow, s_dig, tid, (2u*sp)*cap + gid, (2u*sp + 1u)*cap + gid, nullptr
+    if( valid )
+      a.st_a[ gid ] = (uint8_t)(FD_PIPE_ST_VALID | (desc_ok ? FD_PIPE_ST_DESC : 0) | (bad_s ? FD_PIPE_ST_BADS : 0) |
+                                ((stA & 1) ? FD_PIPE_ST_A_OK : 0) | ((stA & 2) ? FD_PIPE_ST_A_SM : 0) |
+                                (un ? FD_PIPE_ST_UNEG : 0));
 #ifdef FD_PHASE_STAMPS
-                              , nullptr
-#endif
-                              );
-    if( valid ) a.out_prev[ gid ] = (int8_t)code;
-#ifdef FD_PHASE_STAMPS
-    if( args.stamps && (tid & 63) == 0 ) {           /* pipe stamps: [2] second phase cycles per wave, [7] its waves */
-      atomicAdd( &args.stamps[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - pt0) );
-      atomicAdd( &args.stamps[7], 1ull );
-    }
+    if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[5], 1ull ); }
 #endif
     return;
   }
 
-  /* ---- first phase of the current batch ---- */
-  uint64_t nn = args.n;
-  if( (gid & ~(uint64_t)63) >= nn ) return;
-#ifdef FD_PHASE_STAMPS
-  uint64_t qt0 = __builtin_amdgcn_s_memtime();
-#endif
-  bool valid = gid < nn;
-  fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
-  if( valid ) d = args.desc[ gid ];
-  uint64_t asz = args.arena_sz;
-  bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
-                 (uint64_t)d.msg_off + d.msg_sz <= asz;
-  uint32_t lim_dw = (uint32_t)((asz + 3u) >> 2) + 1u;
-  uint32_t sig[ 16 ], pub[ 8 ];
+  /* ---- phases B (batch j-1) and C (batch j-2): one copy of the chain code
+     for both (two copies of its ~30 KB window loop would not share the
+     instruction cache) ---- */
+  uint4 *    buf = s_buf[ role ][ wv ];
+  uint32_t * y   = s_y[ role ][ wv ];
+  bool phb = role == 1;
+  uint64_t nx = phb ? a.n_b : a.n_c;
+  if( (gid & ~(uint64_t)63) >= nx ) return;
+  bool valid = gid < nx;
+  uint64_t set = phb ? a.set_b : a.set_c;
+  uint32_t const * hand = phb ? a.hand_b : a.hand_c;
+  int ps = valid ? (int)(phb ? a.st_b : a.st_c)[ gid ] : 0;
+  int code;
+  if( phb ) {
+    bool desc_ok = (ps & FD_PIPE_ST_DESC) != 0, bad_s = (ps & FD_PIPE_ST_BADS) != 0;
+    int stA = ((ps & FD_PIPE_ST_A_OK) ? 1 : 0) | ((ps & FD_PIPE_ST_A_SM) ? 2 : 0);
+    int stR = 0;
+    if( desc_ok && !bad_s ) {                         /* R = sig[0:32]: decode, small order, table */
+      uint32_t enc[ 8 ];
 #pragma unroll
-  for( int j=0; j<16; j++ ) sig[j] = 0u;
+      for( int j=0; j<8; j++ ) enc[j] = hand[ (uint64_t)(FD_PH_R + j)*cap + gid ];
+      ge_p3 Q;
+      int ok = ge_decode( Q, enc, !args.ref_codes );
+      int sm = ge_affine_small_order( Q );
+      FE_FENCE();
+      if( ok && !sm && (stA & 1) && !(stA & 2) ) vtab_build( args.vtab, vcap, (2u*set + 1u)*cap + gid, Q );
+      stR = (ok ? 1 : 0) | (sm ? 2 : 0);
+      FE_FENCE();
+    }
+    code = verify_precode( args, desc_ok, bad_s, stA, stR );
+    if( valid ) a.code_b[ gid ] = (int8_t)code;
+  } else {
+    code = valid ? (int)a.code_c[ gid ] : 0;
+  }
+  bool run = valid && code == 0;
+  int nw = __builtin_amdgcn_readfirstlane( (int)(phb ? a.nw_b : a.nw_c)[ gid >> 6 ] );
+  int split = max( nw - (int)a.kb, 0 );
+  int hi = phb ? nw : split, lo = phb ? split : 0;
+  ge_p3 acc;
+  if( run ) {
+    hand_to_lds( y, hand, cap, gid, lane, FD_PH_YU, phb ? 16 : 24 );
+    if( phb ) ge_identity( acc );
+    else {
+      uint32_t const * o = a.acc_c + gid;
 #pragma unroll
-  for( int j=0; j<8; j++ ) pub[j] = 0u;
-  if( desc_ok ) {
-    load_words<16>( sig, args.arena, d.sig_off, lim_dw );
-    load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
-  }
-  bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                           /* :157-159 */
-  bool live  = desc_ok && !bad_s;
-  uint8_t * grow = a.dig_cur + gid;
-  verify_prep_digits( grow, cap, tid, live, sig, pub, args, d, lim_dw
-#ifdef FD_PHASE_STAMPS
-                      , nullptr
-#endif
-                      );
-  FE_FENCE();
-#ifdef FD_PHASE_STAMPS
-  uint64_t qt1 = __builtin_amdgcn_s_memtime();
-#endif
-  int stA = 0;
-  if( live ) {
-    ge_p3 Q;
-    int ok = ge_decode( Q, pub, !args.ref_codes );
-    int sm = ge_affine_small_order( Q );
+      for( int j=0; j<10; j++ ) {
+        acc.X.v[j] = o[ (uint64_t)j*cap ]; acc.Y.v[j] = o[ (uint64_t)(10+j)*cap ];
+        acc.Z.v[j] = o[ (uint64_t)(20+j)*cap ]; acc.T.v[j] = o[ (uint64_t)(30+j)*cap ];
+      }
+    }
     FE_FENCE();
-    if( ok && !sm ) vtab_build( args.vtab, args.vtab_cap, (2u*a.set_cur)*cap + gid, Q );
-    stA = (ok ? 1 : 0) | (sm ? 2 : 0);
+    if( hi > lo )
+      chain_seg( acc, buf, y, y + 8*64, lane, (ps & FD_PIPE_ST_UNEG) != 0, args.vtab, vcap,
+                 (2u*set)*cap + gid, (2u*set + 1u)*cap + gid, nw, hi, lo );
     FE_FENCE();
+    if( phb ) {
+      uint32_t * o = a.acc_b + gid;
+#pragma unroll
+      for( int j=0; j<10; j++ ) {
+        o[ (uint64_t)j*cap ] = acc.X.v[j]; o[ (uint64_t)(10+j)*cap ] = acc.Y.v[j];
+        o[ (uint64_t)(20+j)*cap ] = acc.Z.v[j]; o[ (uint64_t)(30+j)*cap ] = acc.T.v[j];
+      }
+    } else {
+      comb_lds( acc, buf, y + 16*64, lane, args.ctab );
+      /* Q == O  <=>  X == 0 and Y == Z (:225-228 on [v]D) */
+      fe dl;
+      int ex = fe_is_zero( acc.X );
+      fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
+      int ey = fe_is_zero( dl );
+      code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+    }
   }
+  if( !phb && valid ) a.out_c[ gid ] = (int8_t)code;
 #ifdef FD_PHASE_STAMPS
-  if( args.stamps && (tid & 63) == 0 ) {             /* pipe stamps: [0] SHA+lattice+digits, [1] decode+table of A */
-    uint64_t qt2 = __builtin_amdgcn_s_memtime();
-    atomicAdd( &args.stamps[0], (unsigned long long)(qt1 - qt0) );
-    atomicAdd( &args.stamps[1], (unsigned long long)(qt2 - qt1) );
-  }
+  if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[phb ? 1 : 0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[phb ? 6 : 7], 1ull ); }
 #endif
-  if( !valid ) return;
-  a.pcode_cur[ gid ] = (int8_t)(FD_PIPE_ST_VALID | (desc_ok ? FD_PIPE_ST_DESC : 0) | (bad_s ? FD_PIPE_ST_BADS : 0) |
-                                ((stA & 1) ? FD_PIPE_ST_A_OK : 0) | ((stA & 2) ? FD_PIPE_ST_A_SM : 0));
 }
 
 /* ------------------------------------------------------------------ SHA-512 batch */

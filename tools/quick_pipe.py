@@ -1,9 +1,12 @@
 """Quick device-resident timing of the pipelined verify (fd_ed25519_gpu_pipe_dev)
-next to the one-batch launch, on config-2-like batches (dev tool).  With
-FD_ED25519_GPU_LIB=tools/bin/libfd_ed25519_gpu_stamps.so the context prints,
-for the pipe kernel, stamp 'prologue' = first phase SHA+lattice+digits,
-'sha' = first phase decodes+tables, 'lattice' = second phase (chain), in
-cycles per wave."""
+next to the one-batch launch, on config-2-like batches (dev tool).
+
+  quick_pipe.py n [plain|pipe|both|split] K
+
+split: each of the three phases alone.  With
+FD_ED25519_GPU_LIB=tools/bin/libfd_ed25519_gpu_stamps.so the context prints
+"stamps raw h0..h7": h0 / h7 = phase C cycles per wave, h1 / h6 = phase B,
+h2 / h5 = phase A (s_memtime)."""
 import sys, os
 import numpy as np
 import torch
@@ -23,21 +26,24 @@ outs = [torch.zeros(n, dtype=torch.int8, device="cuda") for _ in range(2)]
 st = torch.cuda.Stream()
 torch.cuda.set_stream(st)
 if mode == "split":
-    # first phase alone (pipe_dev right after a flush: no pending batch) and
-    # second phase alone (the flush), alternated, each launch timed
+    # each phase alone: phase A (pipe_dev on an empty pipeline), then two
+    # empty drain steps (phase B alone, phase C alone), each launch timed
     ev = []
     for i in range(K + 10):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         e[0].record()
         g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, outs[0].data_ptr(), stream=st.cuda_stream)
         e[1].record()
-        g.pipe_flush_dev(stream=st.cuda_stream)
+        g.pipe_dev(0, 0, 0, 0, 0, stream=st.cuda_stream)
         e[2].record()
+        g.pipe_dev(0, 0, 0, 0, 0, stream=st.cuda_stream)
+        e[3].record()
         ev.append(e)
     torch.cuda.synchronize()
     ev = ev[10:]
-    t1 = np.mean([a.elapsed_time(b) for a, b, c in ev]); t2 = np.mean([b.elapsed_time(c) for a, b, c in ev])
-    print("split n=%d  first phase alone %.3f ms, second phase alone %.3f ms, sum %.3f ms" % (n, t1, t2, t1 + t2), flush=True)
+    t = [np.mean([e[k].elapsed_time(e[k + 1]) for e in ev]) for k in range(3)]
+    print("split n=%d  phase A alone %.3f ms, B alone %.3f ms, C alone %.3f ms, sum %.3f ms" % (n, t[0], t[1], t[2], sum(t)),
+          flush=True)
     g.close()
     sys.exit(0)
 for m in (["plain", "pipe"] if mode == "both" else [mode]):
