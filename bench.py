@@ -110,12 +110,18 @@ def valu_peak():
     return rate * 64 * N_CU * NOMINAL_GHZ * 1e9
 
 
-def pmc_traffic(n):
-    path = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+PROFILE_ROUND = "r02"
+
+
+def pmc_traffic(n, kernel):
+    """HBM bytes per launch of this kernel at this batch size, from the
+    committed PMC summary of this round (tools/profile.sh ->
+    tools/summarize_profile.py), or None."""
+    path = os.path.join(REPO, "profiles", PROFILE_ROUND, "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
-    if d.get("batch") != n:
+    if d.get("batch") != n or d.get("kernel") != kernel:
         return None
     return d.get("hbm_bytes_per_launch")
 
@@ -211,9 +217,11 @@ def main():
                     help="untimed back-to-back steps for this long before the warm-up steps: a GPU that was idle "
                          "runs its first ~100 ms at a ramping clock; the timed region should see the clock a "
                          "continuously fed verify stage runs at (reported as prime_steps)")
-    ap.add_argument("--pipeline", type=int, default=0, choices=[0, 1],
-                    help="1: each step is one fd_ed25519_gpu_pipe_dev launch (this batch's first phase beside the "
-                         "previous batch's second phase: two batches in flight, every launch one batch of work)")
+    ap.add_argument("--pipeline", type=int, default=1, choices=[0, 1],
+                    help="1 (default): each step is one fd_ed25519_gpu_pipe_dev launch (phase A of this batch, "
+                         "B of the previous one, C of the one before: three batches in flight, every launch one "
+                         "batch of work; the drain after the timed steps is timed and reported too); "
+                         "0: each step is one fd_ed25519_gpu_verify_batch_dev launch (the whole batch)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test mode (tests/test_bench_launch.py): gloo, a no-op step on a fixed count; "
                          "exercises the launcher, rank setup and SUM/MAX aggregation without a GPU")
@@ -270,12 +278,12 @@ def main():
     d_out = torch.zeros(n, dtype=torch.int8, device=dev)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    pipe = bool(args.pipeline) and not args.hot_keys and n <= 65536 * 4
+    pipe = bool(args.pipeline) and not args.hot_keys
     d_outs = [d_out, torch.zeros(n, dtype=torch.int8, device=dev)]
     nstep = [0]
 
     def step():
-        if pipe:   # batch i's codes land in d_outs[i % 2] when launch i+1 completes
+        if pipe:   # batch i's codes land in d_outs[i % 2] when launch i+2 completes
             g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, d_outs[nstep[0] & 1].data_ptr(),
                        stream=stream.cuda_stream)
             nstep[0] += 1
@@ -284,12 +292,16 @@ def main():
                            stream=stream.cuda_stream)
 
     def settle():
-        """codes of every launched batch final (pipeline: the pending second phase)"""
+        """codes of every launched batch final (pipeline: the pending phases
+        of the last two batches); returns the drain's wall time in s"""
+        t = time.perf_counter()
         if pipe:
             g.pipe_flush_dev(stream=stream.cuda_stream)
         torch.cuda.synchronize()
+        t = time.perf_counter() - t
         for o in (d_outs if pipe else [d_out]):
             assert np.array_equal(o.cpu().numpy(), expect), "verify codes differ from the expected ones"
+        return t
 
     prime = 0
     t_prime = time.perf_counter()
@@ -314,7 +326,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    settle()
+    drain = settle()
 
     from firedancer_amd.dist import aggregate_throughput
     total, dt_max = aggregate_throughput(n * args.steps, dt, device=dev)
@@ -324,6 +336,11 @@ def main():
                 4: "config4: adversarial golden mix, %d-descriptor batch per GPU, device-resident" % n}[args.config]
     value = total / dt_max
 
+    pair_max = 256 * torch.cuda.get_device_properties(dev).multi_processor_count   # the host's pair_max
+    kname = ("fd_ed25519_verify_pipe_kernel" if pipe else
+             "fd_ed25519_verify_cached_kernel" if args.hot_keys else
+             "fd_ed25519_verify_pair_kernel" if n <= pair_max and os.environ.get("FD_ED25519_GPU_PAIR") != "0"
+             else "fd_ed25519_verify_kernel")
     if rank == 0:
         peak = valu_peak()
         achieved = W_MAC * n / (launch_ms * 1e-3)
@@ -344,18 +361,25 @@ def main():
                        "msg_sz": args.msg_sz if args.config == 2 else None, "parallelism": "shard-per-gpu x%d" % world},
             "roofline": {"bound": "valu-int32", "achieved": achieved / 1e12, "peak": peak / 1e12,
                          "unit": "T MAC/s (32x32->64 multiply-adds, W=%.4g per verify)" % W_MAC,
-                         "frac": achieved / peak, "traffic": pmc_traffic(n) if args.config == 2 and not args.hot_keys else None,
+                         "frac": achieved / peak, "traffic": pmc_traffic(n, kname) if args.config == 2 else None,
                          "kernel_ms": launch_ms},
             "cpu_baseline": None,
             "prime_steps": prime,
         }
         if pipe:
-            line["pipeline"] = ("fd_ed25519_gpu_pipe_dev: each timed step is one launch running this batch's first "
-                                "phase (checks, SHA-512, lattice, decodes, tables) beside the previous batch's second "
-                                "phase (chain, compare); two batches in flight, every launch one batch of work")
+            line["pipeline"] = {
+                "api": "fd_ed25519_gpu_pipe_dev",
+                "note": "each timed step is one launch running phase A (checks, SHA-512, lattice, decode + table "
+                        "of A) of this batch, phase B (decode + table of R, checks, top chain windows) of the "
+                        "previous one and phase C (rest of the chain, [w]B, compare) of the one before: three "
+                        "batches in flight, every launch one batch of work; the batches in flight when the timed "
+                        "region starts were launched in the warm-up, the last two finish in the drain after it",
+                "drain_ms": drain * 1e3,
+                "value_with_drain": n * args.steps / (dt + drain),
+            }
         # The same launch against the HBM roofline (not the bound: ~1/6 of the ~8 TB/s peak),
         # from the PMC-measured bytes per launch of profiles/r01/pmc_traffic.json.
-        t = pmc_traffic(n) if args.config == 2 and not args.hot_keys else None
+        t = pmc_traffic(n, kname) if args.config == 2 else None
         if t:
             gbs = t / (launch_ms * 1e-3) / 1e9
             line["roofline_hbm"] = {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",

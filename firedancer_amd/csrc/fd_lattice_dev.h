@@ -183,9 +183,11 @@ FD_LT_FN int lat_lt( uint32_t const a[ 8 ], uint32_t const b[ 8 ] ) { return !la
 /* 8-word x: word i selected by a lane-varying i in [2, 7] (select chain, no
    dynamic register indexing). */
 FD_LT_FN uint32_t lat_word( uint32_t const x[ 8 ], int i ) {
-  uint32_t r = x[2];
-  r = i == 3 ? x[3] : r; r = i == 4 ? x[4] : r; r = i == 5 ? x[5] : r;
-  r = i == 6 ? x[6] : r; r = i == 7 ? x[7] : r;
+  /* word i (2 <= i <= 7) by masks: a select chain over the array is folded
+     back into an indexed load by the compiler, which puts x in scratch */
+  uint32_t r = 0u;
+#pragma unroll
+  for( int j=2; j<8; j++ ) r |= x[j] & (0u - (uint32_t)(i == j));
   return r;
 }
 

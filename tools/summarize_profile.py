@@ -22,11 +22,11 @@ import statistics
 import sys
 
 
-VERIFY_KERNELS = ("fd_ed25519_verify_pair_kernel", "fd_ed25519_verify_kernel")
+VERIFY_KERNELS = ("fd_ed25519_verify_pipe_kernel", "fd_ed25519_verify_pair_kernel", "fd_ed25519_verify_kernel")
 
 
 def verify_kernel(path):
-    """The verify kernel the profiled bench launched (config 2 takes the pair kernel)."""
+    """The verify kernel the profiled bench launched (config 2: the pipe kernel by default)."""
     names = {r["Kernel_Name"] for r in csv.DictReader(open(path))}
     return next(k for k in VERIFY_KERNELS if k in names)
 
@@ -67,8 +67,12 @@ def main():
     }
     json.dump(traffic, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
 
-    sq = pmc(os.path.join(src, "pmc_sq", "pmc_counter_collection.csv"))[-1]
-    gr = pmc(os.path.join(src, "pmc_grbm", "pmc_counter_collection.csv"))[-1]
+    def mid(rows):   # a steady-state launch (a pipelined run's last launches drain it)
+        return rows[len(rows) // 2]
+    sq = mid(pmc(os.path.join(src, "pmc_sq", "pmc_counter_collection.csv")))
+    gr = mid(pmc(os.path.join(src, "pmc_grbm", "pmc_counter_collection.csv")))
+    iss_path = os.path.join(src, "pmc_issue", "pmc_counter_collection.csv")
+    iss = mid(pmc(iss_path)) if os.path.exists(iss_path) else None
     waves = sq["SQ_WAVES"]
     out = {k: v for k, v in sq.items()}
     out.update({
@@ -80,9 +84,17 @@ def main():
         "cycles_per_valu_instr": 4.0 * sq["SQ_WAVE_CYCLES"] / sq["SQ_INSTS_VALU"],
         "GRBM_GUI_ACTIVE": gr.get("GRBM_GUI_ACTIVE"),
         "effective_clock_ghz": gr.get("GRBM_GUI_ACTIVE", 0) / 8.0 / gr["dur_ns"],
-        "note": "SQ_WAVE_CYCLES / SQ_WAIT_ANY count quad-cycles (x4 = cycles); the pair kernel runs two waves "
-                "per 64 signatures (one exits after the decodes), the single-lane kernel one",
+        "note": "SQ_WAVE_CYCLES / SQ_WAIT_ANY count quad-cycles (x4 = cycles); the pipe kernel runs three "
+                "waves per 64 signatures per launch (phases A, B, C of three batches), the pair kernel two (one "
+                "exits after the decodes), the single-lane kernel one",
     })
+    if iss:
+        out["issue"] = {k: v for k, v in iss.items() if k.startswith("SQ_")}
+        busy = iss.get("SQ_BUSY_CU_CYCLES")
+        if busy:
+            # per SIMD: VALU instructions per busy cycle (SQ_BUSY_CU_CYCLES: quad-cycles per CU, summed)
+            out["issue"]["valu_instr_per_simd_cycle"] = iss["SQ_INSTS_VALU"] / (4.0 * busy * 4.0)
+            out["issue"]["dual_issue_frac"] = iss.get("SQ_ACTIVE_INST_VALU2", 0) / max(iss.get("SQ_ACTIVE_INST_VALU", 1), 1)
     json.dump(out, open(os.path.join(dst, "pmc_sq.json"), "w"), indent=1)
 
     ip = os.path.join(src, "issue_probe.jsonl")
