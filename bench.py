@@ -217,11 +217,13 @@ def main():
                     help="untimed back-to-back steps for this long before the warm-up steps: a GPU that was idle "
                          "runs its first ~100 ms at a ramping clock; the timed region should see the clock a "
                          "continuously fed verify stage runs at (reported as prime_steps)")
-    ap.add_argument("--pipeline", type=int, default=1, choices=[0, 1],
-                    help="1 (default): each step is one fd_ed25519_gpu_pipe_dev launch (phase A of this batch, "
-                         "B of the previous one, C of the one before: three batches in flight, every launch one "
-                         "batch of work; the drain after the timed steps is timed and reported too); "
-                         "0: each step is one fd_ed25519_gpu_verify_batch_dev launch (the whole batch)")
+    ap.add_argument("--pipeline", type=int, default=-1, choices=[-1, 0, 1],
+                    help="1: each step is one fd_ed25519_gpu_pipe_dev launch (phase A of this batch, B of the "
+                         "previous one, C of the one before: three batches in flight, every launch one batch of "
+                         "work; the drain after the timed steps is timed and reported too); 0: each step is one "
+                         "fd_ed25519_gpu_verify_batch_dev launch (the whole batch); -1 (default): 1 when the batch "
+                         "is at most one wave per SIMD (256 x CUs signatures: config 2), else 0 (larger batches "
+                         "already give every SIMD several waves, and the single-lane kernel packs them better)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test mode (tests/test_bench_launch.py): gloo, a no-op step on a fixed count; "
                          "exercises the launcher, rank setup and SUM/MAX aggregation without a GPU")
@@ -278,7 +280,8 @@ def main():
     d_out = torch.zeros(n, dtype=torch.int8, device=dev)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    pipe = bool(args.pipeline) and not args.hot_keys
+    pair_max = 256 * torch.cuda.get_device_properties(dev).multi_processor_count   # the host's pair_max
+    pipe = (args.pipeline == 1 or (args.pipeline == -1 and n <= pair_max)) and not args.hot_keys
     d_outs = [d_out, torch.zeros(n, dtype=torch.int8, device=dev)]
     nstep = [0]
 
@@ -336,7 +339,6 @@ def main():
                 4: "config4: adversarial golden mix, %d-descriptor batch per GPU, device-resident" % n}[args.config]
     value = total / dt_max
 
-    pair_max = 256 * torch.cuda.get_device_properties(dev).multi_processor_count   # the host's pair_max
     kname = ("fd_ed25519_verify_pipe_kernel" if pipe else
              "fd_ed25519_verify_cached_kernel" if args.hot_keys else
              "fd_ed25519_verify_pair_kernel" if n <= pair_max and os.environ.get("FD_ED25519_GPU_PAIR") != "0"
