@@ -143,25 +143,30 @@ int fd_ed25519_verify_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx,
                                      int8_t * d_out, void * stream );
 
 /* Pipelined device-resident verify (throughput form of the entry above).
-   Each call enqueues ONE launch that runs the first phase (descriptor and S
-   checks, SHA-512, lattice split, digits, both decodes and small-order
-   checks, both tables) of this batch beside the second phase (the
-   scalar-multiplication chain and the compare) of the batch passed to the
-   previous call, and writes THAT batch's codes into its d_out.  So codes of
-   batch i are final once call i+1 (or fd_ed25519_gpu_pipe_flush_dev) has
-   completed on the stream, and batch i's buffers (d_arena, d_desc, d_out)
-   must stay valid until then.  Between the phases a batch lives in the
-   slot's pipe scratch (its own two table sets, digit rows and pre-codes, not
-   shared with the other entry points).  Why: one 64-signature wave per SIMD
-   leaves most VALU issue slots empty during the chain; the first phase of
-   the next batch fills them.  desc_cnt <= the context's max_batch (rounded
-   up to 256); a context with hot keys cached is refused (ERR_ARG).  Codes
-   are the same as every other entry point's. */
+   Each call enqueues ONE launch that runs three phases of three batches:
+   phase A of this batch (descriptor and S checks, SHA-512, lattice split,
+   w, decode + small-order check + table of A), phase B of the batch of the
+   previous call (decode + small-order check + table of R, the check-order
+   code, the top windows of the scalar-multiplication chain) and phase C of
+   the batch of the call before that (the rest of the chain, [w]B, the
+   compare), which writes THAT batch's codes into its d_out.  So the codes of
+   batch i are final once call i+2 (or fd_ed25519_gpu_pipe_flush_dev) has
+   completed on the stream; batch i's d_out must stay valid until then, its
+   d_arena and d_desc only until call i's launch has completed (phase A
+   copies what the later phases need).  Between the phases a batch lives in
+   the slot's pipe scratch (three table sets and hand-off records, not shared
+   with the other entry points).  Why: config-2-sized batches are one
+   64-signature wave per SIMD; the three phases give every SIMD three waves.
+   desc_cnt == 0 is a drain step.  desc_cnt <= the context's max_batch
+   (rounded up to 256); a context with hot keys cached is refused (ERR_ARG).
+   Codes are the same as every other entry point's.  Replaces nothing in the
+   reference: the verify tile's fd_txn_verify calls (fd_verify.h:43-88) see
+   the same codes, one batch later. */
 int fd_ed25519_gpu_pipe_dev( fd_ed25519_gpu_t * ctx, int dev_idx,
                              uint8_t const * d_arena, uint64_t arena_sz,
                              fd_ed25519_desc_t const * d_desc, uint64_t desc_cnt,
                              int8_t * d_out, void * stream );
-/* Enqueues the second phase of the pending batch alone (no-op if none). */
+/* Enqueues the drain steps that finish every pending batch (no-op if none). */
 int fd_ed25519_gpu_pipe_flush_dev( fd_ed25519_gpu_t * ctx, int dev_idx, void * stream );
 
 /* Single-signature and single-message-batch drop-ins (host memory, synchronous).
