@@ -93,6 +93,9 @@ def load_lib():
     lib.fd_ed25519_gpu_frags_to_descs.argtypes = [vp, u64, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_verify_frags.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_precompile_verify.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp]
+    lib.fd_ed25519_gpu_gossip_walk.restype = ctypes.c_int64
+    lib.fd_ed25519_gpu_gossip_walk.argtypes = [vp, u64, u64, u64, vp, u64, vp, vp, u64, vp]
+    lib.fd_ed25519_gpu_gossip_verify.argtypes = [vp, vp, u64, u64, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_host_register.argtypes = [vp, vp, u64]
     lib.fd_ed25519_gpu_host_unregister.argtypes = [vp, vp]
     lib.fd_ed25519_gpu_keycache_reserve.argtypes = [vp, u64]
@@ -136,6 +139,24 @@ def pack_batch(records):
         desc[i] = (off, off + 64, off + 96, len(msg), txn)
         off += 96 + len(msg)
     return arena, desc, total
+
+
+GOSSIP_CORRUPT, GOSSIP_UNSIGNED, GOSSIP_NOT_MINE, GOSSIP_CRDS = -110, -111, -112, -113
+
+
+def gossip_walk(arena, arena_sz, aux_off, aux_cap, pkts, self_pubkey=None):
+    """fd_ed25519_gpu_gossip_walk (host, no GPU): -> (desc, pkt_desc)."""
+    lib = load_lib()
+    pkts = np.ascontiguousarray(pkts, dtype=SPAN_DTYPE)
+    n = len(pkts)
+    desc = np.zeros(max(n, 1), DESC_DTYPE)
+    pd = np.zeros(max(n, 1), np.int64)
+    me = None if self_pubkey is None else ctypes.c_char_p(bytes(self_pubkey))
+    nd = lib.fd_ed25519_gpu_gossip_walk(_ptr(arena), arena_sz, aux_off, aux_cap, _ptr(pkts), n, me,
+                                        _ptr(desc), n, _ptr(pd))
+    if nd < 0:
+        raise GpuError("fd_ed25519_gpu_gossip_walk: %s (%d)" % (strerror(int(nd)), nd))
+    return desc[:nd], pd[:n]
 
 
 def txn_reduce(codes, desc):
@@ -298,6 +319,20 @@ class Ed25519Gpu:
         if r:
             raise GpuError("fd_ed25519_gpu_precompile_verify: %s (%d)" % (strerror(r), r))
         return out[:len(instrs)]
+
+    def gossip_verify(self, arena, arena_sz, aux_off, aux_cap, pkts, self_pubkey=None):
+        """Gossip packets (SPAN_DTYPE spans of arena, a writable uint8 array
+        with room for the rebuilt prune messages at [aux_off, aux_off +
+        aux_cap)) -> int32 per packet: the verify code of its signature or
+        a GOSSIP_* walk status (include/fd_ed25519_gpu.h)."""
+        pkts = np.ascontiguousarray(pkts, dtype=SPAN_DTYPE)
+        out = np.zeros(max(len(pkts), 1), np.int32)
+        me = None if self_pubkey is None else ctypes.c_char_p(bytes(self_pubkey))
+        r = self.lib.fd_ed25519_gpu_gossip_verify(self.ctx, _ptr(arena), arena_sz, aux_off, aux_cap, _ptr(pkts),
+                                                  len(pkts), me, _ptr(out))
+        if r:
+            raise GpuError("fd_ed25519_gpu_gossip_verify: %s (%d)" % (strerror(r), r))
+        return out[:len(pkts)]
 
     def sha512_batch(self, msgs):
         """Batched SHA-512 of a list of byte strings (mirror of fd_sha512_batch_add per message)."""

@@ -7,6 +7,7 @@
      fd_verify_stage.cpp    frag -> descriptor parse (host), the tcache, the
                             sync stage and the async stage with host parse
      fd_precompile.cpp      the precompile record walk
+     fd_gossip_verify.cpp   the gossip packet walk (ping / pong / prune)
      fd_verify_offload.cpp  the shared-memory link (client and server sides)
    The GPU entry points those sources call are replaced HERE by a stand-in
    that touches every byte a descriptor names (so an out-of-arena
@@ -249,6 +250,49 @@ static void check_precompile( int iters ) {
   }
 }
 
+/* Gossip packets: well-formed ping / pong / prune layouts (random counts,
+   lengths off by a few bytes) and random bytes, in exact-size arenas with
+   the aux region after them. */
+static uint64_t st_gossip = 0;
+static void check_gossip( int iters ) {
+  for( int it=0; it<iters; it++ ) {
+    std::vector<uint8_t> a; std::vector<fd_ed25519_gpu_span_t> pk;
+    uint64_t np = 1 + rnd( 8 );
+    for( uint64_t j=0; j<np; j++ ) {
+      uint64_t off = a.size(), sz;
+      uint32_t kind = rnd( 4 ) ? (uint32_t)rnd( 7 ) : (uint32_t)rng();
+      if( kind == 4 || kind == 5 ) sz = 132 + (rnd( 3 ) ? 0 : rnd( 5 ) - 2);
+      else if( kind == 3 ) {
+        uint64_t n = rnd( 6 ) ? rnd( 8 ) : rng();
+        sz = 4 + 32 + 32 + 8 + 32 * (n & 15) + 64 + 32 + 8 + (rnd( 3 ) ? 0 : rnd( 5 ) - 2);
+        for( uint64_t i=0; i<sz; i++ ) a.push_back( (uint8_t)rng() );
+        if( sz >= 76 ) memcpy( &a[ off + 68 ], &n, 8 );
+      } else sz = rnd( 300 );
+      if( kind != 3 ) for( uint64_t i=0; i<sz; i++ ) a.push_back( (uint8_t)rng() );
+      if( sz >= 4 ) memcpy( &a[ off ], &kind, 4 );
+      pk.push_back( { (uint32_t)off, (uint32_t)sz } );
+    }
+    uint64_t aux_off = a.size(), aux_cap = aux_off;
+    a.resize( aux_off + aux_cap );
+    exact ar( a );
+    uint8_t me[ 32 ]; memcpy( me, ar.p + (ar.n > 200 ? 100 : 0), 32 <= ar.n ? 32 : 0 );
+    std::vector<fd_ed25519_desc_t> desc( np ); std::vector<int64_t> pd( np );
+    int64_t nd = fd_ed25519_gpu_gossip_walk( ar.p, ar.n, aux_off, aux_cap, pk.data(), np, rnd( 2 ) ? me : NULL,
+                                             desc.data(), np, pd.data() );
+    if( nd < 0 ) { fprintf( stderr, "gossip walk %ld\n", (long)nd ); exit( 1 ); }
+    st_gossip += (uint64_t)nd;
+    std::vector<int8_t> code( nd ? nd : 1 );
+    if( stand_in_verify( ar.p, ar.n, desc.data(), (uint64_t)nd, code.data() ) ) { fprintf( stderr, "gossip desc outside\n" ); exit( 1 ); }
+    std::vector<int> out( np );
+    fd_ed25519_gpu_t ctx; ctx.pend = 0;
+    if( fd_ed25519_gpu_gossip_verify( &ctx, ar.p, ar.n, aux_off, aux_cap, pk.data(), np, me, out.data() ) ) {
+      fprintf( stderr, "gossip_verify\n" ); exit( 1 );
+    }
+    if( fd_ed25519_gpu_gossip_walk( ar.p, ar.n, 0, 4, pk.data(), np, NULL, desc.data(), np, pd.data() ) != FD_ED25519_GPU_ERR_ARG &&
+        pk[ 0 ].sz ) { fprintf( stderr, "aux over a packet accepted\n" ); exit( 1 ); }
+  }
+}
+
 /* The link with a hostile peer: the header is rewritten at random between
    calls, and every call on both sides must stay inside the mapping. */
 static void check_offload( int iters ) {
@@ -304,10 +348,11 @@ int main( int argc, char ** argv ) {
   check_stage( 400 * scale );
   check_tcache( 20000 * scale );
   check_precompile( 3000 * scale );
+  check_gossip( 3000 * scale );
   check_offload( 20000 * scale );
   printf( "sanitize_host: ok (frags: %lu parsed ok, %lu failed, %lu bad, %lu descriptors; precompile %lu descriptors; "
-          "link %lu published, %lu taken, %lu joins refused)\n", (unsigned long)st_ok, (unsigned long)st_failed,
-          (unsigned long)st_bad, (unsigned long)st_desc, (unsigned long)st_walk, (unsigned long)st_pub,
+          "gossip %lu descriptors; link %lu published, %lu taken, %lu joins refused)\n", (unsigned long)st_ok, (unsigned long)st_failed,
+          (unsigned long)st_bad, (unsigned long)st_desc, (unsigned long)st_walk, (unsigned long)st_gossip, (unsigned long)st_pub,
           (unsigned long)st_avail, (unsigned long)st_join_refused );
   return 0;
 }

@@ -33,6 +33,15 @@ Files written (tests/golden/):
                     public_from_private, sign, verify must be SUCCESS), as sig records
                     (set 50), reference codes recorded
 
+  gossip.bin        gossip packets -- the reference's own gossip fixtures
+                    (src/flamenco/types/fixtures/gossip_*.bin: a pull request, pull
+                    responses carrying contact-info v1/v2, node-instance, snapshot-hash
+                    and version values, a push of a vote) plus ping / pong / prune
+                    packets signed by the reference signer and malformed variants --
+                    with the (msg, sig, key, code) triples the REFERENCE gossip code
+                    forms for each (oracle/ref_gossip.c: the reference decoder,
+                    encoder and fd_ed25519_verify)
+
 `python3 make_golden.py cctv_batches.bin fuzz_seeds.bin` rewrites only the named files.
 
 Record format (ed25519 files), little endian:
@@ -42,6 +51,9 @@ txn_batches.bin record:
   u32 n, u32 msg_sz, i8 code_avx512, i8 code_ref, u16 0, u8 sigs[64n], u8 pubs[32n], u8 msg[msg_sz]
 sha512_kat.bin record:
   u32 msg_sz, u8 digest[64], u8 msg[msg_sz]
+gossip.bin: u8 self[32], then per packet:
+  u32 tag, u32 pkt_sz, i32 ntriples (-1: the packet does not decode), u8 pkt[pkt_sz],
+  ntriples x { u32 kind, u32 msg_sz, u8 msg[msg_sz], u8 sig[64], u8 key[32], i32 code }
 """
 import ctypes
 import os
@@ -73,6 +85,9 @@ def load_libs():
                                                       ctypes.c_char_p, ctypes.c_ulong]
         lib.fdref_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
         lib.fdref_public_from_private.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        lib.fdref_gossip_triples.restype = ctypes.c_long
+        lib.fdref_gossip_triples.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p,
+                                             ctypes.c_ulong]
         assert lib.fdref_backend_avx512() == (1 if b == "avx512" else 0)
         libs[b] = lib
     return libs
@@ -335,6 +350,93 @@ def gen_fuzz_seeds():
     return out
 
 
+GOSSIP_SELF = bytes(range(100, 132))
+
+
+def gossip_triples(pkt, me=GOSSIP_SELF):
+    """The reference gossip code's triples for one packet (oracle/ref_gossip.c)."""
+    buf = ctypes.create_string_buffer(1 << 20)
+    n = LIBS["avx512"].fdref_gossip_triples(pkt, len(pkt), me, buf, len(buf))
+    assert n >= -1, n
+    if n < 0:
+        return None
+    out, at = [], 0
+    raw = buf.raw
+    for _ in range(n):
+        kind, msz = struct.unpack_from("<II", raw, at); at += 8
+        msg = raw[at:at + msz]; at += msz
+        sig = raw[at:at + 64]; at += 64
+        key = raw[at:at + 32]; at += 32
+        code, = struct.unpack_from("<i", raw, at); at += 4
+        out.append((kind, msg, sig, key, code))
+    return out
+
+
+def gen_gossip():
+    """Gossip packets and the reference's triples (fd_gossip.c:474-484, 735-762,
+    830-900, 1002-1030 via oracle/ref_gossip.c)."""
+    pkts = []
+    fx = os.path.join(REF_SRC, "flamenco/types/fixtures")
+    for i, name in enumerate(sorted(f for f in os.listdir(fx) if f.startswith("gossip_") and f.endswith(".bin"))):
+        pkts.append((100 + i, open(os.path.join(fx, name), "rb").read()))
+    rng = np.random.default_rng(1589)
+    keys = [keypair(rng) for _ in range(4)]
+    # ping / pong: {u32 kind, from, token, signature}
+    for kind in (4, 5):
+        for t in range(6):
+            priv, pub = keys[t % 4]
+            token = rng.bytes(32)
+            sig = sign(token, pub, priv)
+            p = struct.pack("<I", kind) + pub + token + sig
+            if t == 1:
+                p = p[:100] + bytes([p[100] ^ 4]) + p[101:]          # signature bit flip
+            elif t == 2:
+                p = p[:40] + bytes([p[40] ^ 1]) + p[41:]             # token bit flip
+            elif t == 3:
+                p = p + b"\0"                                       # a byte over
+            elif t == 4:
+                p = p[:-1]                                           # a byte short
+            elif t == 5:
+                p = struct.pack("<I", kind) + rng.bytes(32) + token + sig   # a key that may not decode
+            pkts.append((kind * 10 + t, p))
+
+    def prune(priv, pub, inner, prunes, dest, wall, nfield=None, tail=b""):
+        n = len(prunes) if nfield is None else nfield
+        body = lambda sig: (struct.pack("<I", 3) + pub + inner + struct.pack("<Q", n) + b"".join(prunes) + sig +
+                            dest + struct.pack("<Q", wall) + tail)
+        tr = gossip_triples(body(bytes(64)), me=dest)
+        if not tr:
+            return body(rng.bytes(64))
+        return body(sign(tr[0][1], pub, priv))
+    for t in range(12):
+        priv, pub = keys[t % 4]
+        pr = [rng.bytes(32) for _ in range((0, 1, 3, 20)[t % 4])]
+        wall = int(rng.integers(0, 2**62))
+        inner = pub if t % 3 else keys[(t + 1) % 4][1]
+        if t == 5:
+            p = prune(priv, pub, inner, pr, rng.bytes(32), wall)               # not for this node
+        elif t == 6:
+            p = bytearray(prune(priv, pub, inner, pr, GOSSIP_SELF, wall)); p[-50] ^= 0x10; p = bytes(p)
+        elif t == 7:
+            p = prune(priv, pub, inner, pr, GOSSIP_SELF, wall, nfield=len(pr) + 1)   # count past the data
+        elif t == 8:
+            p = prune(priv, pub, inner, pr, GOSSIP_SELF, wall, nfield=1 << 63)
+        elif t == 9:
+            p = prune(priv, pub, inner, pr, GOSSIP_SELF, wall, tail=b"\1\2")       # bytes over
+        else:
+            p = prune(priv, pub, inner, pr, GOSSIP_SELF, wall)
+        pkts.append((60 + t, p))
+    pkts.append((90, struct.pack("<I", 7) + rng.bytes(128)))                 # unknown kind
+    pkts.append((91, b"\4\0\0"))                                             # short
+    out = [GOSSIP_SELF]
+    for tag, p in pkts:
+        tr = gossip_triples(p)
+        out.append(struct.pack("<IIi", tag, len(p), -1 if tr is None else len(tr)) + p)
+        for kind, msg, sig, key, code in tr or []:
+            out.append(struct.pack("<II", kind, len(msg)) + msg + sig + key + struct.pack("<i", code))
+    return out
+
+
 def gen_sha512(vecs):
     out = []
     for set_id, tc_id, ok, msg, sig, pub in vecs:
@@ -364,7 +466,8 @@ def main():
     vecs = extract_reference_vectors()
     gens = {"vectors_ref.bin": lambda: gen_vectors_ref(vecs), "synthetic.bin": gen_synthetic,
             "txn_batches.bin": gen_txn_batches, "sha512_kat.bin": lambda: gen_sha512(vecs),
-            "cctv_batches.bin": lambda: gen_cctv_batches(vecs), "fuzz_seeds.bin": gen_fuzz_seeds}
+            "cctv_batches.bin": lambda: gen_cctv_batches(vecs), "fuzz_seeds.bin": gen_fuzz_seeds,
+            "gossip.bin": gen_gossip}
     only = sys.argv[1:] or list(gens)
     for name in only:
         recs = gens[name]()

@@ -40,3 +40,22 @@ def read_sha(name="sha512_kat.bin"):
         md = data[off:off + 64]; off += 64
         out.append((data[off:off + sz], md)); off += sz
     return out
+
+
+def read_gossip(name="gossip.bin"):
+    """-> (self_pubkey, list of dict(tag, pkt, triples: None (does not decode) or
+    list of dict(kind, msg, sig, key, code)))."""
+    data = open(os.path.join(GOLDEN, name), "rb").read()
+    me, off, out = data[:32], 32, []
+    while off < len(data):
+        tag, sz, nt = struct.unpack_from("<IIi", data, off); off += 12
+        pkt = data[off:off + sz]; off += sz
+        trs = None if nt < 0 else []
+        for _ in range(max(nt, 0)):
+            kind, msz = struct.unpack_from("<II", data, off); off += 8
+            msg = data[off:off + msz]; off += msz
+            sig = data[off:off + 64]; key = data[off + 64:off + 96]; off += 96
+            (code,) = struct.unpack_from("<i", data, off); off += 4
+            trs.append(dict(kind=kind, msg=msg, sig=sig, key=key, code=code))
+        out.append(dict(tag=tag, pkt=pkt, triples=trs))
+    return me, out
