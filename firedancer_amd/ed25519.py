@@ -96,6 +96,10 @@ def load_lib():
     lib.fd_ed25519_gpu_gossip_walk.restype = ctypes.c_int64
     lib.fd_ed25519_gpu_gossip_walk.argtypes = [vp, u64, u64, u64, vp, u64, vp, vp, u64, vp]
     lib.fd_ed25519_gpu_gossip_verify.argtypes = [vp, vp, u64, u64, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_shred_walk.restype = ctypes.c_int64
+    lib.fd_ed25519_gpu_shred_walk.argtypes = [vp, u64, u64, u64, vp, vp, u64, vp, u64, vp]
+    lib.fd_ed25519_gpu_shred_verify.argtypes = [vp, vp, u64, u64, u64, vp, vp, u64, vp]
+    lib.fd_ed25519_gpu_sha256.argtypes = [vp, u64, vp]
     lib.fd_ed25519_gpu_host_register.argtypes = [vp, vp, u64]
     lib.fd_ed25519_gpu_host_unregister.argtypes = [vp, vp]
     lib.fd_ed25519_gpu_keycache_reserve.argtypes = [vp, u64]
@@ -157,6 +161,31 @@ def gossip_walk(arena, arena_sz, aux_off, aux_cap, pkts, self_pubkey=None):
     if nd < 0:
         raise GpuError("fd_ed25519_gpu_gossip_walk: %s (%d)" % (strerror(int(nd)), nd))
     return desc[:nd], pd[:n]
+
+
+SHRED_PARSE, SHRED_ZERO_SIG, SHRED_COUNTS, SHRED_INDEX, SHRED_DEPTH, SHRED_PROOF = -120, -121, -122, -123, -124, -125
+
+
+def shred_walk(arena, arena_sz, aux_off, aux_cap, shreds, key_off):
+    """fd_ed25519_gpu_shred_walk (host, no GPU): -> (desc, shred_desc)."""
+    lib = load_lib()
+    shreds = np.ascontiguousarray(shreds, dtype=SPAN_DTYPE)
+    key_off = np.ascontiguousarray(key_off, dtype=np.uint32)
+    n = len(shreds)
+    desc = np.zeros(max(n, 1), DESC_DTYPE)
+    sd = np.zeros(max(n, 1), np.int64)
+    nd = lib.fd_ed25519_gpu_shred_walk(_ptr(arena), arena_sz, aux_off, aux_cap, _ptr(shreds), _ptr(key_off), n,
+                                       _ptr(desc), n, _ptr(sd))
+    if nd < 0:
+        raise GpuError("fd_ed25519_gpu_shred_walk: %s (%d)" % (strerror(int(nd)), nd))
+    return desc[:nd], sd[:n]
+
+
+def sha256(msg):
+    lib = load_lib()
+    out = ctypes.create_string_buffer(32)
+    lib.fd_ed25519_gpu_sha256(ctypes.c_char_p(bytes(msg)), len(msg), out)
+    return out.raw
 
 
 def txn_reduce(codes, desc):
@@ -333,6 +362,19 @@ class Ed25519Gpu:
         if r:
             raise GpuError("fd_ed25519_gpu_gossip_verify: %s (%d)" % (strerror(r), r))
         return out[:len(pkts)]
+
+    def shred_verify(self, arena, arena_sz, aux_off, aux_cap, shreds, key_off):
+        """Shreds (SPAN_DTYPE spans of arena) with their leaders' keys at
+        arena[key_off[j]:+32] -> int32 per shred: the verify code of the
+        FEC resolver's root check or a SHRED_* status (include/fd_ed25519_gpu.h)."""
+        shreds = np.ascontiguousarray(shreds, dtype=SPAN_DTYPE)
+        key_off = np.ascontiguousarray(key_off, dtype=np.uint32)
+        out = np.zeros(max(len(shreds), 1), np.int32)
+        r = self.lib.fd_ed25519_gpu_shred_verify(self.ctx, _ptr(arena), arena_sz, aux_off, aux_cap, _ptr(shreds),
+                                                 _ptr(key_off), len(shreds), _ptr(out))
+        if r:
+            raise GpuError("fd_ed25519_gpu_shred_verify: %s (%d)" % (strerror(r), r))
+        return out[:len(shreds)]
 
     def sha512_batch(self, msgs):
         """Batched SHA-512 of a list of byte strings (mirror of fd_sha512_batch_add per message)."""

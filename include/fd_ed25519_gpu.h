@@ -413,6 +413,43 @@ int fd_ed25519_gpu_gossip_verify( fd_ed25519_gpu_t * ctx, uint8_t * arena, uint6
                                   uint64_t aux_cap, fd_ed25519_gpu_span_t const * pkt, uint64_t n,
                                   uint8_t const * self, int * out );
 
+/* ---- Shred leader signatures --------------------
+
+   The check the reference FEC resolver makes on the shred that opens a FEC
+   set (src/disco/shred/fd_fec_resolver.c:309-405): fd_shred_parse
+   (src/ballet/shred/fd_shred.c:4-60), then the resolver's own checks, the
+   Merkle root of the shred's inclusion proof (SHA-256 leaf over the
+   protected region, 20-byte nodes, "SOLANA_MERKLE_SHREDS_{LEAF,NODE}"
+   prefixes), and fd_ed25519_verify( root, 32, signature, leader ).  The host
+   computes the roots (into arena[aux_off, aux_off + 32 n)); one GPU batch
+   verifies.  Which shreds open a set (the resolver's maps) is the caller's
+   state.  Statuses of shreds that are not verified: */
+#define FD_ED25519_GPU_SHRED_PARSE     (-120)   /* fd_shred_parse rejects it (or it is shorter than its leaf region) */
+#define FD_ED25519_GPU_SHRED_ZERO_SIG  (-121)   /* :313 */
+#define FD_ED25519_GPU_SHRED_COUNTS    (-122)   /* coding shred data / code count 0 or > 67, :324-328 */
+#define FD_ED25519_GPU_SHRED_INDEX     (-123)   /* index within its type >= 67, :352-354 */
+#define FD_ED25519_GPU_SHRED_DEPTH     (-124)   /* proof too short for the index, :358 */
+#define FD_ED25519_GPU_SHRED_PROOF     (-125)   /* index past the resolver's 10-layer tree, fd_bmtree.c:394 */
+
+/* Host, no GPU.  Shred j is span shred[j], its leader's public key the 32
+   bytes at arena + key_off[j].  shred_desc[j] = its descriptor's index in
+   desc (msg = its root in aux, txn_idx = j mod 2^16) or a status above.
+   aux must hold 32 bytes per verified shred and not overlap a shred or a
+   key.  Returns the descriptor count or FD_ED25519_GPU_ERR_ARG. */
+int64_t fd_ed25519_gpu_shred_walk( uint8_t * arena, uint64_t arena_sz, uint64_t aux_off, uint64_t aux_cap,
+                                   fd_ed25519_gpu_span_t const * shred, uint32_t const * key_off, uint64_t n,
+                                   fd_ed25519_desc_t * desc, uint64_t desc_cap, int64_t * shred_desc );
+
+/* Walk + one GPU batch: out[j] = the verify code of shred j's signature
+   (FD_ED25519_SUCCESS / FD_ED25519_ERR_*) or its status.  Host memory,
+   synchronous. */
+int fd_ed25519_gpu_shred_verify( fd_ed25519_gpu_t * ctx, uint8_t * arena, uint64_t arena_sz, uint64_t aux_off,
+                                 uint64_t aux_cap, fd_ed25519_gpu_span_t const * shred, uint32_t const * key_off,
+                                 uint64_t n, int * out );
+
+/* SHA-256 (FIPS 180-4) of msg, host; the Merkle hashing above uses it. */
+void fd_ed25519_gpu_sha256( uint8_t const * msg, uint64_t sz, uint8_t out[ 32 ] );
+
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
    u32 words each, k < l) on the context's first device.  out: n records of

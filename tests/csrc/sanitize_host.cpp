@@ -8,6 +8,7 @@
                             sync stage and the async stage with host parse
      fd_precompile.cpp      the precompile record walk
      fd_gossip_verify.cpp   the gossip packet walk (ping / pong / prune)
+     fd_shred_verify.cpp    the shred parse + Merkle root walk
      fd_verify_offload.cpp  the shared-memory link (client and server sides)
    The GPU entry points those sources call are replaced HERE by a stand-in
    that touches every byte a descriptor names (so an out-of-arena
@@ -293,6 +294,49 @@ static void check_gossip( int iters ) {
   }
 }
 
+/* Shreds: plausible headers (Merkle data / code, legacy variants, random
+   proof lengths, counts and indices), sizes around the fixed ones and
+   random bytes, in exact-size arenas with the leader keys and the roots'
+   aux region. */
+static uint64_t st_shred = 0;
+static void check_shreds( int iters ) {
+  for( int it=0; it<iters; it++ ) {
+    std::vector<uint8_t> a; std::vector<fd_ed25519_gpu_span_t> sp; std::vector<uint32_t> ko;
+    uint64_t n = 1 + rnd( 6 );
+    for( uint64_t j=0; j<n; j++ ) {
+      ko.push_back( (uint32_t)a.size() ); for( int i=0; i<32; i++ ) a.push_back( (uint8_t)rng() );
+      static uint8_t const vs[ 6 ] = { 0x80, 0x40, 0xa5, 0x5a, 0x90, 0x00 };
+      uint8_t variant = (uint8_t)(vs[ rnd( 6 ) ] | (rnd( 4 ) ? (uint8_t)rnd( 16 ) : 0));
+      uint64_t sz = rnd( 5 ) ? ((variant & 0x40) ? 1228 : 1203) + rnd( 9 ) - 4 : rnd( 1300 );
+      uint64_t off = a.size();
+      for( uint64_t i=0; i<sz; i++ ) a.push_back( (uint8_t)rng() );
+      if( sz > 0x40 ) a[ off + 0x40 ] = variant;
+      if( sz > 0x58 ) {
+        uint16_t v16 = (uint16_t)(rnd( 2 ) ? rnd( 70 ) : rng());
+        memcpy( &a[ off + 0x53 ], &v16, 2 ); v16 = (uint16_t)rnd( 70 ); memcpy( &a[ off + 0x55 ], &v16, 2 );
+        v16 = (uint16_t)(rnd( 2 ) ? rnd( 1300 ) : rng()); memcpy( &a[ off + 0x56 ], &v16, 2 );
+        uint32_t fec = (uint32_t)rnd( 100 ), idx = fec + (uint32_t)rnd( 80 ) - 5;
+        memcpy( &a[ off + 0x49 ], &idx, 4 ); memcpy( &a[ off + 0x4f ], &fec, 4 );
+      }
+      sp.push_back( { (uint32_t)off, (uint32_t)sz } );
+    }
+    uint64_t aux_off = a.size(), aux_cap = 32 * n;
+    a.resize( aux_off + aux_cap );
+    exact ar( a );
+    std::vector<fd_ed25519_desc_t> desc( n ); std::vector<int64_t> sd( n );
+    int64_t nd = fd_ed25519_gpu_shred_walk( ar.p, ar.n, aux_off, aux_cap, sp.data(), ko.data(), n, desc.data(), n, sd.data() );
+    if( nd < 0 ) { fprintf( stderr, "shred walk %ld\n", (long)nd ); exit( 1 ); }
+    st_shred += (uint64_t)nd;
+    std::vector<int8_t> code( nd ? nd : 1 );
+    if( stand_in_verify( ar.p, ar.n, desc.data(), (uint64_t)nd, code.data() ) ) { fprintf( stderr, "shred desc outside\n" ); exit( 1 ); }
+    std::vector<int> out( n );
+    fd_ed25519_gpu_t ctx; ctx.pend = 0;
+    if( fd_ed25519_gpu_shred_verify( &ctx, ar.p, ar.n, aux_off, aux_cap, sp.data(), ko.data(), n, out.data() ) ) {
+      fprintf( stderr, "shred_verify\n" ); exit( 1 );
+    }
+  }
+}
+
 /* The link with a hostile peer: the header is rewritten at random between
    calls, and every call on both sides must stay inside the mapping. */
 static void check_offload( int iters ) {
@@ -349,10 +393,12 @@ int main( int argc, char ** argv ) {
   check_tcache( 20000 * scale );
   check_precompile( 3000 * scale );
   check_gossip( 3000 * scale );
+  check_shreds( 1500 * scale );
   check_offload( 20000 * scale );
   printf( "sanitize_host: ok (frags: %lu parsed ok, %lu failed, %lu bad, %lu descriptors; precompile %lu descriptors; "
-          "gossip %lu descriptors; link %lu published, %lu taken, %lu joins refused)\n", (unsigned long)st_ok, (unsigned long)st_failed,
-          (unsigned long)st_bad, (unsigned long)st_desc, (unsigned long)st_walk, (unsigned long)st_gossip, (unsigned long)st_pub,
+          "gossip %lu descriptors; shreds %lu descriptors; link %lu published, %lu taken, %lu joins refused)\n",
+          (unsigned long)st_ok, (unsigned long)st_failed, (unsigned long)st_bad, (unsigned long)st_desc, (unsigned long)st_walk,
+          (unsigned long)st_gossip, (unsigned long)st_shred, (unsigned long)st_pub,
           (unsigned long)st_avail, (unsigned long)st_join_refused );
   return 0;
 }

@@ -42,6 +42,12 @@ Files written (tests/golden/):
                     forms for each (oracle/ref_gossip.c: the reference decoder,
                     encoder and fd_ed25519_verify)
 
+  shreds.bin        shreds -- the 480 of the reference's demo capture
+                    (src/disco/shred/fixtures/demo-shreds.pcap, leader key
+                    demo-shreds.key) plus corrupted variants -- with the result of
+                    the REFERENCE FEC resolver's first-shred check (oracle/ref_shred.c:
+                    the reference fd_shred_parse, bmtree, SHA-256, fd_ed25519_verify)
+
 `python3 make_golden.py cctv_batches.bin fuzz_seeds.bin` rewrites only the named files.
 
 Record format (ed25519 files), little endian:
@@ -51,6 +57,9 @@ txn_batches.bin record:
   u32 n, u32 msg_sz, i8 code_avx512, i8 code_ref, u16 0, u8 sigs[64n], u8 pubs[32n], u8 msg[msg_sz]
 sha512_kat.bin record:
   u32 msg_sz, u8 digest[64], u8 msg[msg_sz]
+shreds.bin record:
+  u32 tag, u32 sz, i32 result (verify code, or -101..-106 as oracle/ref_shred.c), u8 root[32],
+  u8 leader[32], u8 shred[sz]
 gossip.bin: u8 self[32], then per packet:
   u32 tag, u32 pkt_sz, i32 ntriples (-1: the packet does not decode), u8 pkt[pkt_sz],
   ntriples x { u32 kind, u32 msg_sz, u8 msg[msg_sz], u8 sig[64], u8 key[32], i32 code }
@@ -85,6 +94,8 @@ def load_libs():
                                                       ctypes.c_char_p, ctypes.c_ulong]
         lib.fdref_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
         lib.fdref_public_from_private.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        lib.fdref_shred_check.restype = ctypes.c_int
+        lib.fdref_shred_check.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
         lib.fdref_gossip_triples.restype = ctypes.c_long
         lib.fdref_gossip_triples.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p,
                                              ctypes.c_ulong]
@@ -437,6 +448,71 @@ def gen_gossip():
     return out
 
 
+def shred_check(sh, leader):
+    """the reference FEC resolver's first-shred check (oracle/ref_shred.c)"""
+    root = ctypes.create_string_buffer(32)
+    r = LIBS["avx512"].fdref_shred_check(sh, len(sh), leader, root)
+    return r, (root.raw if r > -100 else bytes(32))
+
+
+def gen_shreds():
+    """The reference's demo shred capture (fd_fec_resolver tests' fixtures)
+    and corrupted variants, with the reference resolver's check."""
+    d = os.path.join(REF_SRC, "disco/shred/fixtures")
+    leader = open(os.path.join(d, "demo-shreds.key"), "rb").read()[32:]
+    cap = open(os.path.join(d, "demo-shreds.pcap"), "rb").read()
+    shreds, off = [], 24
+    while off < len(cap):
+        incl, = struct.unpack_from("<I", cap, off + 8); off += 16
+        shreds.append(cap[off + 42:off + incl]); off += incl      # Ethernet + IPv4 + UDP headers
+    rng = np.random.default_rng(399)
+    other = keypair(rng)[1]
+    recs = [(i, sh, leader) for i, sh in enumerate(shreds)]
+
+    def put16(b, o, v):
+        b[o:o + 2] = struct.pack("<H", v & 0xffff)
+
+    def put32(b, o, v):
+        b[o:o + 4] = struct.pack("<I", v & 0xffffffff)
+    data = [sh for sh in shreds if sh[0x40] & 0xf0 == 0x80]
+    code = [sh for sh in shreds if sh[0x40] & 0xf0 == 0x40]
+    for t in range(48):
+        base = bytearray((data if t % 2 else code)[int(rng.integers(0, 240))])
+        k = t // 2
+        if k == 0:   base[100 + int(rng.integers(0, 900))] ^= 1                      # protected byte
+        elif k == 1: base[len(base) - 1 - int(rng.integers(0, 20 * (base[0x40] & 0xf)))] ^= 0x40   # proof byte
+        elif k == 2: base[0:64] = bytes(64)                                          # zero signature
+        elif k == 3: base[5] ^= 0x80                                                 # signature bit
+        elif k == 4: base[32:64] = (L + int(rng.integers(0, 1000))).to_bytes(32, "little")   # S >= l
+        elif k == 5: base = base[:-1]                                                # a byte short
+        elif k == 6: base[0x40] = (base[0x40] & 0xf0) | ((base[0x40] + 1) & 0xf)    # proof length + 1
+        elif k == 7: base[0x40] = (base[0x40] & 0xf0) | ((base[0x40] - 1) & 0xf)    # proof length - 1
+        elif k == 8: base[0x40] = (base[0x40] & 0xf0)                                # no proof
+        elif k == 9: base[0x40] = 0x5a if t % 2 == 0 else 0x20 | (base[0x40] & 0xf)  # legacy code / bad type
+        elif k == 10:
+            if t % 2: put32(base, 0x49, struct.unpack_from("<I", base, 0x4f)[0] - 1)    # idx below its set
+            else: put16(base, 0x53, 0)                                                # data count 0
+        elif k == 11:
+            if t % 2: put32(base, 0x49, struct.unpack_from("<I", base, 0x4f)[0] + 66)  # index 66: deeper than the proof
+            else: put16(base, 0x53, 68)                                               # data count 68
+        elif k == 12:
+            if t % 2: put16(base, 0x56, 0x50)                                         # data size below the header
+            else: put16(base, 0x55, 0)                                                # code count 0
+        elif k == 13:
+            if t % 2: base = base + bytes(25)                                         # extra bytes after a data shred
+            else: put16(base, 0x57, 67)                                               # coding index 67
+        elif k == 14: base = base + bytes(3)                                          # bytes over
+        elif k == 15: recs.append((1000 + t, bytes(base), other)); continue           # another leader
+        elif k == 16: base[0x41] ^= 1                                                  # slot (unprotected? no: in the leaf)
+        else: base[64 + int(rng.integers(0, 0x18))] ^= 0x10                          # header bytes
+        recs.append((1000 + t, bytes(base), leader))
+    out = []
+    for tag, sh, ld in recs:
+        r, root = shred_check(sh, ld)
+        out.append(struct.pack("<IIi", tag, len(sh), r) + root + ld + sh)
+    return out
+
+
 def gen_sha512(vecs):
     out = []
     for set_id, tc_id, ok, msg, sig, pub in vecs:
@@ -467,7 +543,7 @@ def main():
     gens = {"vectors_ref.bin": lambda: gen_vectors_ref(vecs), "synthetic.bin": gen_synthetic,
             "txn_batches.bin": gen_txn_batches, "sha512_kat.bin": lambda: gen_sha512(vecs),
             "cctv_batches.bin": lambda: gen_cctv_batches(vecs), "fuzz_seeds.bin": gen_fuzz_seeds,
-            "gossip.bin": gen_gossip}
+            "gossip.bin": gen_gossip, "shreds.bin": gen_shreds}
     only = sys.argv[1:] or list(gens)
     for name in only:
         recs = gens[name]()

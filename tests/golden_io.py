@@ -59,3 +59,14 @@ def read_gossip(name="gossip.bin"):
             trs.append(dict(kind=kind, msg=msg, sig=sig, key=key, code=code))
         out.append(dict(tag=tag, pkt=pkt, triples=trs))
     return me, out
+
+
+def read_shreds(name="shreds.bin"):
+    """-> list of dict(tag, result, root, leader, shred) (shreds.bin: make_golden.py gen_shreds)."""
+    data = open(os.path.join(GOLDEN, name), "rb").read()
+    out, off = [], 0
+    while off < len(data):
+        tag, sz, r = struct.unpack_from("<IIi", data, off); off += 12
+        root = data[off:off + 32]; leader = data[off + 32:off + 64]; off += 64
+        out.append(dict(tag=tag, result=r, root=root, leader=leader, shred=data[off:off + sz])); off += sz
+    return out

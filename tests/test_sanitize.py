@@ -1,8 +1,8 @@
 """CPU: AddressSanitizer + UndefinedBehaviorSanitizer over the host code that
 parses attacker-shaped bytes: the frag ->
 descriptor parse, the tcache, the sync and async verify stages (host parse),
-the precompile record walk, the gossip packet walk and the offload
-shared-memory link.
+the precompile record walk, the gossip packet walk, the shred walk and the
+offload shared-memory link.
 
 1. tests/csrc/sanitize_host.cpp: those product sources compiled with
    -fsanitize=address,undefined and driven with random / corrupted frags,
@@ -36,7 +36,7 @@ def test_sanitized_driver():
     import re
     nums = [int(x) for x in re.findall(r"(\d+) (?:parsed ok|failed|bad|descriptors|published|taken|joins refused)",
                                         r.stdout)]
-    assert len(nums) == 9 and min(nums) > 0, r.stdout
+    assert len(nums) == 10 and min(nums) > 0, r.stdout
 
 
 def test_cpu_suites_against_asan_libraries():
@@ -52,7 +52,7 @@ def test_cpu_suites_against_asan_libraries():
                ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
                FD_ED25519_GPU_LIB=gpu_lib, FD_VERIFY_OFFLOAD_LIB=off_lib)
     suites = ["tests/test_offload.py", "tests/test_abi.py", "tests/test_verify_stage.py", "tests/test_precompile.py",
-              "tests/test_gossip.py"]
+              "tests/test_gossip.py", "tests/test_shred.py"]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "not gpu", "-p", "no:cacheprovider"] + suites,
                        cwd=REPO, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
