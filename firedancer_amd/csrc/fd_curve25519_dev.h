@@ -56,19 +56,19 @@ FD_FN void ge_identity( ge_p3 & p ) { fe_set0( p.X ); fe_set1( p.Y ); fe_set1( p
    not fit 32 bits, its x2 does, and F x M column sums stay below 2^63),
    which drops one fe_carry per doubling / mixed addition. */
 FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
-  fe XX, YY, ZZ, AA, s, H, G, E, Fn;
+  fe XX, YY, ZZ, s, H, G, E, Fn;
   fe_sq( XX, p.X );                     /* R */
   FE_FENCE();
   fe_sq( YY, p.Y );                     /* R */
   FE_FENCE();
   fe_sq( ZZ, p.Z );                     /* R */
   FE_FENCE();
+  fe_add( H, YY, XX );                  /* M   H = YY+XX, not carried: first operand only */
+  fe_sub4p( G, H );                     /*     4p - H, the addend that subtracts H        */
   fe_add( s, p.X, p.Y );                /* M */
-  fe_sq( AA, s );                       /* R */
+  fe_sq_seed( E, s, G );                /* R   E = (X+Y)^2-YY-XX = 2XY, carried by the square */
   FE_FENCE();
-  fe_add_r( H, YY, XX );                /* R   H = YY+XX          */
   fe_sub( G, YY, XX );                  /* M   G = YY-XX          */
-  fe_sub( E, AA, H );                   /* M   E = (X+Y)^2-YY-XX = 2XY */
   fe_add( s, ZZ, ZZ ); fe_add( s, s, XX );
   fe_sub( Fn, s, YY );                  /* F   Fn = 2ZZ-G, not carried: first operand only */
   fe_mul( r.X, Fn, E );

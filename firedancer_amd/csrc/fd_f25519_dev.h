@@ -26,7 +26,8 @@
    (e.g. 2R + R + 2p - R uncarried): fe_mul( h, F, M ) is exact with h in R
    (2*F fits 32 bits, column sums < 2^62.9); 19*F does not fit, so an F value
    is never the second operand of fe_mul nor an fe_sq input.
-   fe_mul / fe_sq accept M inputs and return R; fe_add of two R is M;
+   fe_mul / fe_sq accept M inputs and return R; fe_sq_seed( h, f, s ) = f^2 + s
+   likewise (s limbs < 2^31); fe_add of two R is M;
    fe_sub(R, R) is M; fe_carry(any limbs < 2^31) is R. */
 
 #ifndef FD_F25519_DEV_H
@@ -96,6 +97,17 @@ FD_FN void fe_carry( fe & r, fe const & a ) {
 
 FD_FN void fe_add_r( fe & r, fe const & a, fe const & b ) { fe t; fe_add( t, a, b ); fe_carry( r, t ); }
 FD_FN void fe_sub_r( fe & r, fe const & a, fe const & b ) { fe t; fe_sub( t, a, b ); fe_carry( r, t ); }
+
+/* 4p - a, limbwise nonnegative for a up to 2R (a in M from a sum of two R);
+   the addend of fe_sq_seed that subtracts a */
+#define FE_4P0  (4u*(0x3ffffffu-18u))
+#define FE_4PE  (4u*0x3ffffffu)
+#define FE_4PO  (4u*0x1ffffffu)
+FD_FN void fe_sub4p( fe & r, fe const & a ) {
+  r.v[0] = FE_4P0 - a.v[0];
+#pragma unroll
+  for( int i=1; i<10; i++ ) r.v[i] = ((i&1) ? FE_4PO : FE_4PE) - a.v[i];
+}
 
 /* 2p - a (a in R) -> M */
 FD_FN void fe_neg( fe & r, fe const & a ) {
@@ -176,6 +188,40 @@ FD_FN void fe_sq( fe & h, fe const & f ) {
   a = mad64( f0_2,f8, col5( a, f1_2,f7_2, f2_2,f6, f3_2,f5_2, f4,f4, f9,f9_38 ) );
   FE_COL_DONE( a, h8, 26, FE_M26 );
   a = col5( a, f0_2,f9, f1_2,f8, f2_2,f7, f3_2,f6, f4_2,f5 );
+  FE_COL_DONE( a, h9, 25, FE_M25 );
+  a = mad64( (uint32_t)a, 19u, ((uint64_t)(19u*(uint32_t)(a>>32))<<32) | (uint64_t)h0 );
+  h0 = (uint32_t)a & FE_M26;
+  h1 += (uint32_t)(a >> 26);
+  h.v[0]=h0; h.v[1]=h1; h.v[2]=h2; h.v[3]=h3; h.v[4]=h4; h.v[5]=h5; h.v[6]=h6; h.v[7]=h7; h.v[8]=h8; h.v[9]=h9;
+}
+
+/* h = f^2 + s (s limbwise, < 2^31 each, added to each column before its
+   carry).  Input f in M, output in R. */
+FD_FN void fe_sq_seed( fe & h, fe const & f, fe const & s ) {
+  uint32_t f0=f.v[0],f1=f.v[1],f2=f.v[2],f3=f.v[3],f4=f.v[4],f5=f.v[5],f6=f.v[6],f7=f.v[7],f8=f.v[8],f9=f.v[9];
+  uint32_t f0_2=2u*f0, f1_2=2u*f1, f2_2=2u*f2, f3_2=2u*f3, f4_2=2u*f4, f5_2=2u*f5, f6_2=2u*f6, f7_2=2u*f7;
+  uint32_t f5_38=38u*f5, f6_19=19u*f6, f7_38=38u*f7, f8_19=19u*f8, f9_38=38u*f9;
+  uint64_t a;
+  uint32_t h0,h1,h2,h3,h4,h5,h6,h7,h8,h9;
+  a = col5( (uint64_t)f0*f0 + s.v[0], f1_2,f9_38, f2_2,f8_19, f3_2,f7_38, f4_2,f6_19, f5,f5_38 );
+  FE_COL_DONE( a, h0, 26, FE_M26 );
+  a = col5( a + s.v[1], f0_2,f1, f2,f9_38, f3_2,f8_19, f4,f7_38, f5_2,f6_19 );
+  FE_COL_DONE( a, h1, 25, FE_M25 );
+  a = mad64( f0_2,f2, col5( a + s.v[2], f1_2,f1, f3_2,f9_38, f4_2,f8_19, f5_2,f7_38, f6,f6_19 ) );
+  FE_COL_DONE( a, h2, 26, FE_M26 );
+  a = col5( a + s.v[3], f0_2,f3, f1_2,f2, f4,f9_38, f5_2,f8_19, f6,f7_38 );
+  FE_COL_DONE( a, h3, 25, FE_M25 );
+  a = mad64( f0_2,f4, col5( a + s.v[4], f1_2,f3_2, f2,f2, f5_2,f9_38, f6_2,f8_19, f7,f7_38 ) );
+  FE_COL_DONE( a, h4, 26, FE_M26 );
+  a = col5( a + s.v[5], f0_2,f5, f1_2,f4, f2_2,f3, f6,f9_38, f7_2,f8_19 );
+  FE_COL_DONE( a, h5, 25, FE_M25 );
+  a = mad64( f0_2,f6, col5( a + s.v[6], f1_2,f5_2, f2_2,f4, f3_2,f3, f7_2,f9_38, f8,f8_19 ) );
+  FE_COL_DONE( a, h6, 26, FE_M26 );
+  a = col5( a + s.v[7], f0_2,f7, f1_2,f6, f2_2,f5, f3_2,f4, f8,f9_38 );
+  FE_COL_DONE( a, h7, 25, FE_M25 );
+  a = mad64( f0_2,f8, col5( a + s.v[8], f1_2,f7_2, f2_2,f6, f3_2,f5_2, f4,f4, f9,f9_38 ) );
+  FE_COL_DONE( a, h8, 26, FE_M26 );
+  a = col5( a + s.v[9], f0_2,f9, f1_2,f8, f2_2,f7, f3_2,f6, f4_2,f5 );
   FE_COL_DONE( a, h9, 25, FE_M25 );
   a = mad64( (uint32_t)a, 19u, ((uint64_t)(19u*(uint32_t)(a>>32))<<32) | (uint64_t)h0 );
   h0 = (uint32_t)a & FE_M26;

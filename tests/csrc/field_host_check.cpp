@@ -5,6 +5,8 @@
 extern "C" {
 void t_mul( uint32_t * h, uint32_t const * f, uint32_t const * g ) { fe a, b, r; for( int i=0;i<10;i++ ){a.v[i]=f[i];b.v[i]=g[i];} fe_mul( r, a, b ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
 void t_sq ( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_sq( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_sq_seed( uint32_t * h, uint32_t const * f, uint32_t const * g ) { fe a, b, r; for( int i=0;i<10;i++ ){a.v[i]=f[i];b.v[i]=g[i];} fe_sq_seed( r, a, b ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_sub4p( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_sub4p( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
 void t_sub( uint32_t * h, uint32_t const * f, uint32_t const * g ) { fe a, b, r; for( int i=0;i<10;i++ ){a.v[i]=f[i];b.v[i]=g[i];} fe_sub( r, a, b ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
 void t_carry( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_carry( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
 void t_tobytes( uint32_t * o, uint32_t const * f ) { fe a; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_tobytes32( o, a ); }

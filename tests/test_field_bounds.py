@@ -77,6 +77,26 @@ def test_mul_uncarried_first_operand(lib):
     assert all(x <= (F_E if i % 2 == 0 else F_O) for i, x in enumerate(fm))
 
 
+def test_sq_seed_doubling_e(lib):
+    """ge_dbl's E = (X+Y)^2 - (XX+YY): H = XX + YY left uncarried (2R, a
+    first operand only), the square seeded with 4p - H per column
+    (fe_sq_seed, fd_curve25519_dev.h) -- exact, and E comes out in R."""
+    rng = random.Random(11)
+    r = [R_E if i % 2 == 0 else R_O for i in range(10)]
+    for it in range(3000):
+        mode = "max" if it < 20 else "rand"
+        x = limbs_at(R_E, R_O, mode, rng); y = limbs_at(R_E, R_O, mode, rng)
+        hh = [x[i] + y[i] for i in range(10)]                     # XX + YY, both R
+        assert all(v <= (M_E if i % 2 == 0 else M_O) for i, v in enumerate(hh))
+        sd = (ctypes.c_uint32 * 10)(); lib.t_sub4p(sd, arr(hh)); sd = list(sd)
+        assert all(0 <= v < 2**31 for v in sd) and val(sd) % P == (-val(hh)) % P
+        f = limbs_at(M_E, M_O, mode, rng)                          # X + Y: M
+        h = (ctypes.c_uint32 * 10)(); lib.t_sq_seed(h, arr(f), arr(sd)); h = list(h)
+        assert val(h) % P == (val(f) ** 2 - val(hh)) % P and in_R(h)
+    # the largest H the formula forms still leaves 4p - H nonnegative
+    sd = (ctypes.c_uint32 * 10)(); lib.t_sub4p(sd, arr([2 * v for v in r])); assert all(v < 2**31 for v in sd)
+
+
 def test_sub_carry_canon(lib):
     rng = random.Random(2)
     for it in range(3000):

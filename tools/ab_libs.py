@@ -4,7 +4,10 @@ the same device-resident 64K config-2 batch (65,536 distinct keys, 200-B
 messages); prints the median ms per launch of each and checks that both
 builds return the same codes.
 
-  python3 tools/ab_libs.py A.so B.so [n]
+  python3 tools/ab_libs.py A.so B.so [C.so ...] [n]
+
+AB_MODE=pipe times fd_ed25519_gpu_pipe_dev launches (the bench's step) instead
+of the one-shot fd_ed25519_verify_batch_gpu_dev (codes checked after a flush).
 """
 import ctypes
 import os
@@ -18,8 +21,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402  (the bench's own synthetic workload)
 
-libs = sys.argv[1:3]
-n = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
+libs = [a for a in sys.argv[1:] if a.endswith(".so")]
+n = int(sys.argv[-1]) if not sys.argv[-1].endswith(".so") else 65536
 arena, desc, sz, expect, _ = bench.build_workload(n, 200, seed=0, n_keys=None)
 d_arena = torch.from_numpy(arena).cuda()
 d_desc = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
@@ -33,15 +36,20 @@ for p in libs:
     lib.fd_ed25519_gpu_new.restype = vp
     lib.fd_ed25519_gpu_new.argtypes = [u64, u64]
     lib.fd_ed25519_verify_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_pipe_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_pipe_flush_dev.argtypes = [vp, i32, vp]
     c = lib.fd_ed25519_gpu_new(1, n)
     assert c, p
     ctx.append((lib, c))
 
 
+PIPE = os.environ.get("AB_MODE") == "pipe"
+
+
 def launch(k):
     lib, c = ctx[k]
-    r = lib.fd_ed25519_verify_batch_gpu_dev(c, 0, d_arena.data_ptr(), sz, d_desc.data_ptr(), n,
-                                            outs[k].data_ptr(), st.cuda_stream)
+    f = lib.fd_ed25519_gpu_pipe_dev if PIPE else lib.fd_ed25519_verify_batch_gpu_dev
+    r = f(c, 0, d_arena.data_ptr(), sz, d_desc.data_ptr(), n, outs[k].data_ptr(), st.cuda_stream)
     assert r == 0, r
 
 
@@ -59,8 +67,14 @@ for rnd in range(14):
             b.record(st)
         torch.cuda.synchronize()
         times[k] += [a.elapsed_time(b) for a, b in ev]
+if PIPE:
+    for lib, c in ctx:
+        assert lib.fd_ed25519_gpu_pipe_flush_dev(c, 0, st.cuda_stream) == 0
+    torch.cuda.synchronize()
 for k, p in enumerate(libs):
-    assert np.array_equal(outs[k].cpu().numpy(), expect), p
+    # tools/bin/lib_x*.so: diagnostic builds with wrong results by design (timing only)
+    if not os.path.basename(p).startswith("lib_x"):
+        assert np.array_equal(outs[k].cpu().numpy(), expect), p
     t = sorted(times[k])
     print("%-50s median %.4f ms (%.2f M verifies/s) p10 %.4f p90 %.4f" % (
         os.path.basename(p), statistics.median(t), n / statistics.median(t) / 1e3, t[len(t) // 10], t[9 * len(t) // 10]),

@@ -42,10 +42,13 @@ SQ_TERMS = [
 MUL_INS = ["f%d" % i for i in range(10)] + ["g%d" % i for i in range(10)] + \
           ["g%d_19" % i for i in range(1, 10)] + ["f%d_2" % i for i in (1, 3, 5, 7, 9)]
 SQ_INS = ["f%d" % i for i in range(10)] + ["f%d_2" % i for i in range(8)] + ["f5_38", "f6_19", "f7_38", "f8_19", "f9_38"]
+SEEDS = ["s%d" % i for i in range(10)]
 
 
-def stream(cols, ins, out_base, in_base):
-    """instruction list (strings) of one product"""
+def stream(cols, ins, out_base, in_base, seeds=None):
+    """instruction list (strings) of one product; seeds: per-column 32-bit
+    addends (input names), each added to its column's accumulator by one
+    v_mad_u64_u32 with multiplier 1 before the column's carry moves on"""
     idx = {n: in_base + i for i, n in enumerate(ins)}
     ops = []
     for k, terms in enumerate(cols):
@@ -55,6 +58,8 @@ def stream(cols, ins, out_base, in_base):
         for n, (a, b) in enumerate(terms):
             src2 = "0" if (k == 0 and n == 0) else "%%%d" % o
             ops.append("v_mad_u64_u32 %%%d, vcc, %%%d, %%%d, %s" % (o, idx[a], idx[b], src2))
+        if seeds:
+            ops.append("v_mad_u64_u32 %%%d, vcc, %%%d, 1, %%%d" % (o, idx[seeds[k]], o))
     return ops
 
 
@@ -135,6 +140,15 @@ __device__ __forceinline__ void fe_finish( fe & h, uint64_t c0, uint64_t c1, uin
     out.append("__device__ __forceinline__ void fe_sq( fe & h, fe const & f ) {\n")
     out.append(pre(PRE_SQ, "", "f"))
     out.append(asm_block(stream(SQ_TERMS, SQ_INS, 0, 10), ["c%d" % i for i in range(10)], SQ_INS))
+    out.append(FIN.replace("{H}", "h").replace("{p}", ""))
+    out.append("}\n\n")
+    # fe_sq_seed
+    out.append("/* h = f^2 + s (limbwise addend s, limbs < 2^31, added to each column before\n"
+               "   its carry: h comes out carried).  Input f in M, output in R. */\n")
+    out.append("__device__ __forceinline__ void fe_sq_seed( fe & h, fe const & f, fe const & s ) {\n")
+    out.append(pre(PRE_SQ, "", "f"))
+    out.append("  uint32_t " + ", ".join("s%d=s.v[%d]" % (i, i) for i in range(10)) + ";\n")
+    out.append(asm_block(stream(SQ_TERMS, SQ_INS + SEEDS, 0, 10, seeds=SEEDS), ["c%d" % i for i in range(10)], SQ_INS + SEEDS))
     out.append(FIN.replace("{H}", "h").replace("{p}", ""))
     out.append("}\n\n")
     # fe_mul2

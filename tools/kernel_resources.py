@@ -17,7 +17,7 @@ import sys
 import yaml
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ASM = os.path.join(REPO, "firedancer_amd", "build", "prod", "kern.opt.s")
+ASM = os.environ.get('KR_ASM') or os.path.join(REPO, 'firedancer_amd', 'build', 'prod', 'kern.opt.s')
 VGPR_FILE, VGPR_GRANULE, LDS_CU, MAX_WAVES, SIMDS_PER_CU, CUS = 512, 8, 160 * 1024, 8, 4, 256
 
 
