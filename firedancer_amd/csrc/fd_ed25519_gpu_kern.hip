@@ -625,26 +625,31 @@ __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t co
   }
 }
 
-/* acc += [w]B: the 16 comb-table additions, w's biased digits in yw. */
+/* acc += [w]B: the 16 comb-table additions, w's biased digits in yw.
+   (FD_DIAG_COMB_POS < FD_CTAB_POS: diagnostic build, wrong results, timing
+   of fewer comb additions.) */
+#ifndef FD_DIAG_COMB_POS
+#define FD_DIAG_COMB_POS FD_CTAB_POS
+#endif
 __device__ __forceinline__ void comb_lds( ge_p3 & acc, uint4 * buf, uint32_t const * yw, int lane, uint32_t const * ctab ) {
 #define FD_WDIG( k ) ((int)((yw[ ((k) >> 1)*64 + lane ] >> (16*((k) & 1))) & 0xffffu) - ((k) < FD_CTAB_POS-1 ? 32768 : 0))
   int d = FD_WDIG( 0 );
   ctab_fetch_lds( buf, ctab, 0, d );
 #pragma unroll 1
-  for( int k=0; k<FD_CTAB_POS; k++ ) {
+  for( int k=0; k<FD_DIAG_COMB_POS; k++ ) {
     ge_precomp bp;
     {
       dma_wait();
       uint32_t w[ 32 ];
       lds_words<8>( w, buf, lane );
-      int dn = k + 1 < FD_CTAB_POS ? FD_WDIG( k + 1 ) : 0;
+      int dn = k + 1 < FD_DIAG_COMB_POS ? FD_WDIG( k + 1 ) : 0;
       FE_FENCE();
-      if( k + 1 < FD_CTAB_POS ) ctab_fetch_lds( buf, ctab, k + 1, dn );
+      if( k + 1 < FD_DIAG_COMB_POS ) ctab_fetch_lds( buf, ctab, k + 1, dn );
       ctab_finish( bp, w, d );
       d = dn;
     }
     FE_FENCE();
-    ge_madd( acc, acc, bp, k + 1 < FD_CTAB_POS );
+    ge_madd( acc, acc, bp, k + 1 < FD_DIAG_COMB_POS );
     FE_FENCE();
   }
 #undef FD_WDIG
