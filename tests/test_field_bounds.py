@@ -163,3 +163,30 @@ def test_sha512_block(lib):
     w = arr([0x8000000000000000] + [0] * 15, ctypes.c_uint64)
     lib.t_sha_block(h, w)
     assert b"".join(struct.pack(">Q", v) for v in h) == hashlib.sha512(b"").digest()
+
+
+def test_lattice_short_vector_host(lib):
+    """fd_lattice_dev.h compiled for the host: on random and structured k the
+    search returns u = v k (mod 8l), v odd, 0 < v < l (what makes
+    [v]([S]B - [k]A - R) == O equivalent to the reference's equation) with
+    |u|, |v| around 2^128 (what the chain's window count is sized for; the
+    bounds of the device test, test_gpu_parity.py)."""
+    rng = random.Random(9)
+    ks = [rng.randrange(LL) for _ in range(20000)]
+    ks += [0, 1, 2, 3, LL - 1, LL - 2, 2**128 - 1, 2**128, 2**128 + 1, 2**127, 2**200, 2**252,
+           (8 * LL // 3) % LL, (8 * LL // 5) % LL, 2**64, 12345]
+    ks += [rng.randrange(1 << rng.randrange(1, 253)) for _ in range(2000)]
+    n8, bits = 8 * LL, []
+    u, v, un = (ctypes.c_uint32 * 8)(), (ctypes.c_uint32 * 8)(), ctypes.c_int()
+    for k in ks:
+        it = lib.t_lattice(arr([(k >> (32 * j)) & 0xffffffff for j in range(8)]), u, v, ctypes.byref(un))
+        assert it < 1024, k                                      # not the (k, 1) fallback
+        uu = val32(u) * (-1 if un.value else 1)
+        vv = val32(v)
+        assert vv % 2 == 1 and 0 < vv < LL and (uu - vv * k) % n8 == 0, (k, uu, vv)
+        bits.append(max(abs(uu).bit_length(), vv.bit_length()))
+    assert max(bits[:20000]) <= 140 and sorted(bits[:20000])[19800] <= 131
+
+
+def val32(w):
+    return sum(int(x) << (32 * i) for i, x in enumerate(w))
