@@ -68,9 +68,9 @@ FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
   fe_add( s, p.X, p.Y );                /* M */
   fe_sq_seed( E, s, G );                /* R   E = (X+Y)^2-YY-XX = 2XY, carried by the square */
   FE_FENCE();
-  fe_sub( G, YY, XX );                  /* M   G = YY-XX          */
-  fe_add( s, ZZ, ZZ ); fe_add( s, s, XX );
-  fe_sub( Fn, s, YY );                  /* F   Fn = 2ZZ-G, not carried: first operand only */
+  fe_sub( G, YY, XX );                  /* M   G = YY-XX+2p       */
+  fe_sub4p( s, G );                     /*     4p-G = XX-YY+2p limbwise (G < 4p per limb) */
+  fe_lshl1_add( Fn, ZZ, s );            /* F   Fn = 2ZZ-G, not carried: first operand only */
   fe_mul( r.X, Fn, E );
   FE_FENCE();
   fe_mul( r.Y, H, G );

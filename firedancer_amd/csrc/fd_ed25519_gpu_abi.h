@@ -19,6 +19,12 @@
 #define FD_CTAB_WORDS     ((uint64_t)FD_CTAB_POS * FD_CTAB_N * FD_CTAB_STRIDE)   /* 67 MB */
 #define FD_VTAB_N         9            /* [0..8](-Q), Q = A or R                      */
 #define FD_VTAB_WORDS     40           /* u32 per entry (4 fe)                        */
+/* Word of limb j of field f (0: Y+X, 1: Y-X, 2: 2dT, 3: 2Z) in a variable-
+   base table entry (the comb and key tables keep plain order): Y+X and Y-X interleaved two
+   limbs at a time (16-B chunk c = Y+X limbs 2c, 2c+1 then Y-X limbs 2c,
+   2c+1), so the digit's sign, which swaps them, is an 8-byte offset of the
+   reader's LDS address; 2dT and 2Z follow in order. */
+#define FD_VW( f, j )     ((f) < 2 ? 4*((j) >> 1) + 2*(f) + ((j) & 1) : 10*(f) + (j))
 #define FD_NDIG_MAX       64           /* 4-bit windows of a <= 256-bit scalar        */
 
 /* Hot-key cache (per device): for each cached public key A, the comb table

@@ -185,7 +185,9 @@ __device__ __forceinline__ void vtab_ptrs( uint32_t const * vtab, uint64_t cap, 
 __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint64_t t, int e, ge_cached const & c ) {
   uint32_t w[ 40 ];
 #pragma unroll
-  for( int j=0; j<10; j++ ) { w[j] = c.YpX.v[j]; w[10+j] = c.YmX.v[j]; w[20+j] = c.T2d.v[j]; w[30+j] = c.Z2.v[j]; }
+  for( int j=0; j<10; j++ ) {
+    w[FD_VW(0,j)] = c.YpX.v[j]; w[FD_VW(1,j)] = c.YmX.v[j]; w[FD_VW(2,j)] = c.T2d.v[j]; w[FD_VW(3,j)] = c.Z2.v[j];
+  }
   uint4 const * mc; uint4 const * tc;
   vtab_ptrs( vtab, cap, t, (uint32_t)e, &mc, &tc );
   uint4 * m = (uint4 *)mc; uint4 * tl = (uint4 *)tc;
@@ -232,12 +234,12 @@ __device__ __forceinline__ void vtab_finish( ge_cached & c, uint32_t const w[ 40
   bool neg = db < 8u;
   fe tv, tn;
 #pragma unroll
-  for( int j=0; j<10; j++ ) { tv.v[j] = w[20+j]; c.Z2.v[j] = w[30+j]; }
+  for( int j=0; j<10; j++ ) { tv.v[j] = w[FD_VW(2,j)]; c.Z2.v[j] = w[FD_VW(3,j)]; }
   fe_neg( tn, tv );
 #pragma unroll
   for( int j=0; j<10; j++ ) {
-    c.YpX.v[j] = neg ? w[10+j] : w[j];
-    c.YmX.v[j] = neg ? w[j]    : w[10+j];
+    c.YpX.v[j] = neg ? w[FD_VW(1,j)] : w[FD_VW(0,j)];
+    c.YmX.v[j] = neg ? w[FD_VW(0,j)] : w[FD_VW(1,j)];
     c.T2d.v[j] = neg ? tn.v[j] : tv.v[j];
   }
 }
@@ -548,6 +550,39 @@ __device__ __forceinline__ void lds_words( uint32_t w[ 4*N ], uint4 const * buf,
   for( int j=0; j<N; j++ ) { uint4 v = buf[ 64*j + lane ]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
 }
 
+/* A table entry (NC = 10 16-B chunks) out of the wave's LDS buffer with the
+   digit's sign applied to Y+X / Y-X by the read address (FD_VW: chunk c < 5
+   holds two limbs of each, 8 bytes apart): w gets Y+X, Y-X (already swapped
+   for a negative digit), then 2dT and 2Z in plain order (words 20..39).
+   (The comb and key tables keep the plain order: their VGPR readers'
+   selects between two words of one 16-B load were compiled into dynamic
+   indexing, +1.2K instructions per comb addition in the pair kernel.) */
+template<int NC>
+__device__ __forceinline__ void lds_entry_words( uint32_t w[ 4*NC ], uint4 const * buf, int lane, bool neg ) {
+  char const * b = (char const *)(buf + lane);
+  uint32_t sp = neg ? 8u : 0u;
+  uint2 const * pp = (uint2 const *)(b + sp);
+  uint2 const * pm = (uint2 const *)(b + (8u - sp));
+#pragma unroll
+  for( int c=0; c<5; c++ ) {
+    uint2 x = pp[ c*128 ]; w[2*c] = x.x; w[2*c+1] = x.y;
+    uint2 y = pm[ c*128 ]; w[10+2*c] = y.x; w[11+2*c] = y.y;
+  }
+#pragma unroll
+  for( int j=5; j<NC; j++ ) { uint4 v = buf[ 64*j + lane ]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
+}
+
+/* The cached entry from lds_entry_words' words: 2dT negated for a negative
+   digit (Y+X / Y-X came swapped). */
+__device__ __forceinline__ void lds_entry_finish( ge_cached & c, uint32_t const w[ 40 ], bool neg ) {
+  fe tv, tn;
+#pragma unroll
+  for( int j=0; j<10; j++ ) { c.YpX.v[j] = w[j]; c.YmX.v[j] = w[10+j]; tv.v[j] = w[20+j]; c.Z2.v[j] = w[30+j]; }
+  fe_neg( tn, tv );
+#pragma unroll
+  for( int j=0; j<10; j++ ) c.T2d.v[j] = neg ? tn.v[j] : tv.v[j];
+}
+
 /* Biased 4-bit digit i (0..16) of a recoded scalar y = x + 8 (16^0 + ... +
    16^(nw-2)) held in the wave's LDS column block y[8][64]: nibble i is
    d_i + 8 below the top window and d_i at the top one (recode4_lds's
@@ -601,11 +636,11 @@ __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t co
     {
       dma_wait();
       uint32_t w[ 40 ];
-      lds_words<10>( w, buf, lane );
+      lds_entry_words<10>( w, buf, lane, dba < 8u );
       dbr = ydig( yv, lane, i, nw, false );
       FE_FENCE();
       vtab_fetch_lds( buf, vtab, cap, tr, dbr );     /* LDS reads issued before the DMA see the old bytes */
-      vtab_finish( q, w, dba );
+      lds_entry_finish( q, w, dba < 8u );
     }
     FE_FENCE();
     ge_add_cached( acc, acc, q, true );
@@ -613,11 +648,11 @@ __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t co
     {
       dma_wait();
       uint32_t w[ 40 ];
-      lds_words<10>( w, buf, lane );
+      lds_entry_words<10>( w, buf, lane, dbr < 8u );
       if( i > lo ) dba = ydig( yu, lane, i-1, nw, uneg );
       FE_FENCE();
       if( i > lo ) vtab_fetch_lds( buf, vtab, cap, ta, dba );
-      vtab_finish( q, w, dbr );
+      lds_entry_finish( q, w, dbr < 8u );
     }
     FE_FENCE();
     ge_add_cached( acc, acc, q, i == lo );
@@ -920,6 +955,8 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
 #define FD_PIPE_ST_A_OK   0x04      /* A decodes                              */
 #define FD_PIPE_ST_A_SM   0x08      /* A has small order                      */
 #define FD_PIPE_ST_UNEG   0x10      /* the lattice u is negated               */
+#define FD_PIPE_ST_R_OK   0x20      /* R decodes (FD_PIPE_R_IN_A builds)      */
+#define FD_PIPE_ST_R_SM   0x40      /* R has small order (FD_PIPE_R_IN_A)     */
 
 /* The wave's digit scalars (words [w0, w0 + nwords) of the hand-off, row
    stride cap) into its LDS column block y[nwords][64]. */
@@ -1010,9 +1047,24 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       stA = (ok ? 1 : 0) | (sm ? 2 : 0);
       FE_FENCE();
     }
+    int stR = 0;
+#ifdef FD_PIPE_R_IN_A   /* experiment: R's decode and table in phase A instead of B */
+    if( live ) {
+      uint32_t enc[ 8 ];
+      load_words<8>( enc, args.arena, d.sig_off, lim_dw );
+      ge_p3 Q;
+      int ok = ge_decode( Q, enc, !args.ref_codes );
+      int sm = ge_affine_small_order( Q );
+      FE_FENCE();
+      if( ok && !sm && (stA & 1) && !(stA & 2) ) vtab_build( args.vtab, vcap, (2u*a.set_a + 1u)*cap + gid, Q );
+      stR = (ok ? 1 : 0) | (sm ? 2 : 0);
+      FE_FENCE();
+    }
+#endif
     if( valid )
       a.st_a[ gid ] = (uint8_t)(FD_PIPE_ST_VALID | (desc_ok ? FD_PIPE_ST_DESC : 0) | (bad_s ? FD_PIPE_ST_BADS : 0) |
                                 ((stA & 1) ? FD_PIPE_ST_A_OK : 0) | ((stA & 2) ? FD_PIPE_ST_A_SM : 0) |
+                                ((stR & 1) ? FD_PIPE_ST_R_OK : 0) | ((stR & 2) ? FD_PIPE_ST_R_SM : 0) |
                                 (un ? FD_PIPE_ST_UNEG : 0));
 #ifdef FD_PHASE_STAMPS
     if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[5], 1ull ); }
@@ -1036,7 +1088,8 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   if( phb ) {
     bool desc_ok = (ps & FD_PIPE_ST_DESC) != 0, bad_s = (ps & FD_PIPE_ST_BADS) != 0;
     int stA = ((ps & FD_PIPE_ST_A_OK) ? 1 : 0) | ((ps & FD_PIPE_ST_A_SM) ? 2 : 0);
-    int stR = 0;
+    int stR = ((ps & FD_PIPE_ST_R_OK) ? 1 : 0) | ((ps & FD_PIPE_ST_R_SM) ? 2 : 0);
+#ifndef FD_PIPE_R_IN_A
     if( desc_ok && !bad_s ) {                         /* R = sig[0:32]: decode, small order, table */
       uint32_t enc[ 8 ];
 #pragma unroll
@@ -1049,6 +1102,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       stR = (ok ? 1 : 0) | (sm ? 2 : 0);
       FE_FENCE();
     }
+#endif
     code = verify_precode( args, desc_ok, bad_s, stA, stR );
     if( valid ) a.code_b[ gid ] = (int8_t)code;
   } else {

@@ -109,6 +109,19 @@ FD_FN void fe_sub4p( fe & r, fe const & a ) {
   for( int i=1; i<10; i++ ) r.v[i] = ((i&1) ? FE_4PO : FE_4PE) - a.v[i];
 }
 
+/* r = 2a + b limbwise, one v_lshl_add_u32 per limb on the device (as asm:
+   the compiler would otherwise reassociate the sum into two adds). */
+FD_FN void fe_lshl1_add( fe & r, fe const & a, fe const & b ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm( "v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r.v[i]) : "v"(a.v[i]), "v"(b.v[i]) );
+#else
+    r.v[i] = (a.v[i] << 1) + b.v[i];
+#endif
+  }
+}
+
 /* 2p - a (a in R) -> M */
 FD_FN void fe_neg( fe & r, fe const & a ) {
   r.v[0] = FE_2P0 - a.v[0];

@@ -73,6 +73,20 @@ def test_mul_uncarried_first_operand(lib):
     two_p = [2 * (2**26 - 19)] + [2 * (2**26 - 1) if i % 2 == 0 else 2 * (2**25 - 1) for i in range(1, 10)]
     fn = [3 * r[i] + two_p[i] for i in range(10)]            # 2ZZ + XX + 2p - 0
     assert all(x <= (F_E if i % 2 == 0 else F_O) for i, x in enumerate(fn))
+    # ge_dbl forms Fn as 2 ZZ + (4p - G), G = YY - XX + 2p: 4p - G stays
+    # nonnegative per limb at G's largest value (YY = R, XX = 0), and the sum
+    # is limbwise the same 2ZZ + XX - YY + 2p
+    sd = (ctypes.c_uint32 * 10)(); lib.t_sub4p(sd, arr([r[i] + two_p[i] for i in range(10)])); sd = list(sd)
+    assert all(0 <= v < 2**31 for v in sd)
+    for it in range(2000):
+        zz = limbs_at(R_E, R_O, "max" if it < 5 else "rand", rng)
+        xx = limbs_at(R_E, R_O, "max" if it < 5 else "rand", rng)
+        yy = limbs_at(R_E, R_O, "max" if it < 5 else "rand", rng)
+        g = [yy[i] + two_p[i] - xx[i] for i in range(10)]
+        sd = (ctypes.c_uint32 * 10)(); lib.t_sub4p(sd, arr(g)); sd = list(sd)
+        fn2 = [2 * zz[i] + sd[i] for i in range(10)]
+        assert fn2 == [2 * zz[i] + xx[i] + two_p[i] - yy[i] for i in range(10)]
+        assert all(x <= (F_E if i % 2 == 0 else F_O) for i, x in enumerate(fn2))
     fm = [2 * r[i] + two_p[i] for i in range(10)]            # 2Z + 2p - 0
     assert all(x <= (F_E if i % 2 == 0 else F_O) for i, x in enumerate(fm))
 
