@@ -371,8 +371,8 @@ def main():
         if pipe:
             line["pipeline"] = {
                 "api": "fd_ed25519_gpu_pipe_dev",
-                "note": "each timed step is one launch running phase A (checks, SHA-512, lattice, decode + table "
-                        "of A) of this batch, phase B (decode + table of R, checks, top chain windows) of the "
+                "note": "each timed step is one launch running phase A (checks, SHA-512, lattice) of this batch, "
+                        "phase B (decode + table of A and of R, check codes, top chain windows) of the "
                         "previous one and phase C (rest of the chain, [w]B, compare) of the one before: three "
                         "batches in flight, every launch one batch of work; the batches in flight when the timed "
                         "region starts were launched in the warm-up, the last two finish in the drain after it",

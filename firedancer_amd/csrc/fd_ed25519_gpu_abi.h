@@ -72,15 +72,14 @@ struct verify_args {
 };
 
 /* Pipelined verify (fd_ed25519_verify_pipe_kernel): one launch runs phase
-   A (checks, SHA-512, lattice, w, decode and table of A) of batch j, phase B
-   (decode and table of R, the check-order code, the top kb windows of the
-   chain) of batch j-1 and phase C (the other windows, [w]B, the compare) of
-   batch j-2.  Between launches a batch lives in HBM, in the set its phase A
+   A (checks, SHA-512, lattice, w) of batch j, phase B (decode and table of A
+   and of R, the check-order code, the top kb windows of the chain) of batch
+   j-1 and phase C (the other windows, [w]B, the compare) of batch j-2.  Between launches a batch lives in HBM, in the set its phase A
    was given (3 sets, batches in flight take different ones):
      tables: A of slot g at table (2 s) sig_cap + g, R at (2 s + 1) sig_cap + g
        of v.vtab (v.vtab_cap = 6 sig_cap);
-     hand-off words [FD_PH_WORDS][sig_cap] (R's encoding, the biased digit
-       scalars), a status byte per slot (FD_PIPE_ST_* bits,
+     hand-off words [FD_PH_WORDS][sig_cap] (R's and A's encodings, the
+       biased digit scalars), a status byte per slot (FD_PIPE_ST_* bits,
        fd_ed25519_gpu_kern.hip), the window count per 64-slot wave;
    and from phase B to phase C (2 sets): the partial sum [FD_PACC_WORDS][sig_cap]
    and the code of the checks per slot.  The arena and descriptors are read by
@@ -89,7 +88,8 @@ struct verify_args {
 #define FD_PH_YU          8            /* u + 8 (16^0 + ... + 16^(nw-2)), 8 words      */
 #define FD_PH_YV          16           /* v + the same bias, 8 words                   */
 #define FD_PH_YW          24           /* w + 2^15 (2^0 + ... + 2^224), 8 words        */
-#define FD_PH_WORDS       32
+#define FD_PH_A           32           /* A's encoding, 8 words                        */
+#define FD_PH_WORDS       40
 #define FD_PACC_WORDS     40           /* X, Y, Z, T                                   */
 #define FD_PIPE_SETS      3
 struct pipe_args {

@@ -930,21 +930,26 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
    768-thread workgroups (waves i, i+4, i+8 share SIMD i: three waves per
    SIMD, none of them idle):
      waves 8-11 (phase A), batch j:   descriptor / S checks, SHA-512, lattice
-       vector (u, v), w = v S mod l, decode A, small-order A, A's table;
-     waves 4-7  (phase B), batch j-1: decode R, small-order R, R's table, the
-       check-order code, then the TOP kb windows of the Straus chain;
+       vector (u, v), w = v S mod l;
+     waves 4-7  (phase B), batch j-1: decode A, small-order A, A's table,
+       decode R, small-order R, R's table, the check-order code, then the
+       TOP kb windows of the Straus chain;
      waves 0-3  (phase C), batch j-2: the remaining windows, the 16 comb
        additions of [w]B and the compare.
-   Why: config 2 is one 64-signature wave per SIMD, and one wave issues at
-   most one VALU instruction per ~4.4 cycles while the SIMD takes more from
-   other waves (tools/fe_probe2.hip: 1.40x the doubling throughput at two
-   waves, 1.75x at four).  Splitting the work of a signature over three
-   launches gives every SIMD three independent waves of similar length.
-   A batch crosses the launches in HBM: phase A leaves R's encoding, the
-   digit scalars (u, v, w plus their recoding bias, so each consumer reads
-   its signed digits straight off the bits) and a status byte per slot and
-   the window count per wave; phase B leaves the partial sum (X, Y, Z, T)
-   and the code of the checks.  The chain phases stage their table entries
+   Why: config 2 is one 64-signature wave per SIMD; a single wave issues a
+   VALU instruction per ~4.6 cycles, the SIMD takes one per ~4.05 from
+   several (tools/fe_probe2.hip, profiles/r02/probes).  The SIMD's arbiter
+   serves the oldest wave first, so the phases run nearly one after the
+   other (C, then B, then A in the leftover issue slots) and the launch ends
+   with the last one alone (profiles/r02/s3/stamps_*): phase A -- the
+   youngest wave, whose code waits on memory most -- is kept short (A's
+   decode and table moved to phase B: -1.6 %; R's moved to phase A instead:
+   +4.8 %).
+   A batch crosses the launches in HBM: phase A leaves R's and A's
+   encodings, the digit scalars (u, v, w plus their recoding bias, so each
+   consumer reads its signed digits straight off the bits), a status byte
+   per slot and the window count per wave; phase B leaves the partial sum
+   (X, Y, Z, T) and the code of the checks.  The chain phases stage their table entries
    in LDS by LDS-DMA (global_load_lds_dwordx4), one entry ahead, instead
    of in 40 VGPRs: 168 VGPRs are the budget of three waves per SIMD.  Same
    device functions and check order as fd_ed25519_verify_kernel:
@@ -952,11 +957,7 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
 #define FD_PIPE_ST_VALID  0x80      /* phase A status byte                    */
 #define FD_PIPE_ST_DESC   0x01      /* descriptor inside the arena            */
 #define FD_PIPE_ST_BADS   0x02      /* S >= l                                 */
-#define FD_PIPE_ST_A_OK   0x04      /* A decodes                              */
-#define FD_PIPE_ST_A_SM   0x08      /* A has small order                      */
 #define FD_PIPE_ST_UNEG   0x10      /* the lattice u is negated               */
-#define FD_PIPE_ST_R_OK   0x20      /* R decodes (FD_PIPE_R_IN_A builds)      */
-#define FD_PIPE_ST_R_SM   0x40      /* R has small order (FD_PIPE_R_IN_A)     */
 
 /* The wave's digit scalars (words [w0, w0 + nwords) of the hand-off, row
    stride cap) into its LDS column block y[nwords][64]. */
@@ -1034,37 +1035,13 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       ybias16( y, w );
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YW + j)*cap ] = y[j];
+#pragma unroll
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_A + j)*cap ] = pub[j];
     }
     if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)nw;
     FE_FENCE();
-    int stA = 0;
-    if( live ) {
-      ge_p3 Q;
-      int ok = ge_decode( Q, pub, !args.ref_codes );
-      int sm = ge_affine_small_order( Q );
-      FE_FENCE();
-      if( ok && !sm ) vtab_build( args.vtab, vcap, (2u*a.set_a)*cap + gid, Q );
-      stA = (ok ? 1 : 0) | (sm ? 2 : 0);
-      FE_FENCE();
-    }
-    int stR = 0;
-#ifdef FD_PIPE_R_IN_A   /* experiment: R's decode and table in phase A instead of B */
-    if( live ) {
-      uint32_t enc[ 8 ];
-      load_words<8>( enc, args.arena, d.sig_off, lim_dw );
-      ge_p3 Q;
-      int ok = ge_decode( Q, enc, !args.ref_codes );
-      int sm = ge_affine_small_order( Q );
-      FE_FENCE();
-      if( ok && !sm && (stA & 1) && !(stA & 2) ) vtab_build( args.vtab, vcap, (2u*a.set_a + 1u)*cap + gid, Q );
-      stR = (ok ? 1 : 0) | (sm ? 2 : 0);
-      FE_FENCE();
-    }
-#endif
     if( valid )
       a.st_a[ gid ] = (uint8_t)(FD_PIPE_ST_VALID | (desc_ok ? FD_PIPE_ST_DESC : 0) | (bad_s ? FD_PIPE_ST_BADS : 0) |
-                                ((stA & 1) ? FD_PIPE_ST_A_OK : 0) | ((stA & 2) ? FD_PIPE_ST_A_SM : 0) |
-                                ((stR & 1) ? FD_PIPE_ST_R_OK : 0) | ((stR & 2) ? FD_PIPE_ST_R_SM : 0) |
                                 (un ? FD_PIPE_ST_UNEG : 0));
 #ifdef FD_PHASE_STAMPS
     if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[5], 1ull ); }
@@ -1087,9 +1064,19 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   int code;
   if( phb ) {
     bool desc_ok = (ps & FD_PIPE_ST_DESC) != 0, bad_s = (ps & FD_PIPE_ST_BADS) != 0;
-    int stA = ((ps & FD_PIPE_ST_A_OK) ? 1 : 0) | ((ps & FD_PIPE_ST_A_SM) ? 2 : 0);
-    int stR = ((ps & FD_PIPE_ST_R_OK) ? 1 : 0) | ((ps & FD_PIPE_ST_R_SM) ? 2 : 0);
-#ifndef FD_PIPE_R_IN_A
+    int stA = 0, stR = 0;
+    if( desc_ok && !bad_s ) {                         /* A: decode, small order, table */
+      uint32_t enc[ 8 ];
+#pragma unroll
+      for( int j=0; j<8; j++ ) enc[j] = hand[ (uint64_t)(FD_PH_A + j)*cap + gid ];
+      ge_p3 Q;
+      int ok = ge_decode( Q, enc, !args.ref_codes );
+      int sm = ge_affine_small_order( Q );
+      FE_FENCE();
+      if( ok && !sm ) vtab_build( args.vtab, vcap, (2u*set)*cap + gid, Q );
+      stA = (ok ? 1 : 0) | (sm ? 2 : 0);
+      FE_FENCE();
+    }
     if( desc_ok && !bad_s ) {                         /* R = sig[0:32]: decode, small order, table */
       uint32_t enc[ 8 ];
 #pragma unroll
@@ -1102,7 +1089,6 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       stR = (ok ? 1 : 0) | (sm ? 2 : 0);
       FE_FENCE();
     }
-#endif
     code = verify_precode( args, desc_ok, bad_s, stA, stR );
     if( valid ) a.code_b[ gid ] = (int8_t)code;
   } else {
