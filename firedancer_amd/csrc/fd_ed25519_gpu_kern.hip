@@ -209,9 +209,11 @@ __device__ __forceinline__ void vtab_build( uint32_t * vtab, uint64_t cap, uint6
   { fe x; fe_neg( x, Q.X ); fe_carry( nQ.X, x ); fe_neg( x, Q.T ); fe_carry( nQ.T, x ); }
   ge_cached c;
   ge_to_cached( c, nQ );  vtab_store( vtab, cap, t, 1, c );   /* d = 0: the shared identity record */
+  /* -Q's affine form for the mixed additions is the cached entry without 2Z:
+     Y+X and Y-X uncarried (M: ge_madd takes them only as second operands of
+     fe_mul), 2dT the same product */
   ge_precomp nQp;
-  { fe d2; fe_const_d2( d2 ); fe_add_r( nQp.YpX, nQ.Y, nQ.X ); fe_sub_r( nQp.YmX, nQ.Y, nQ.X ); fe_mul( nQp.T2d, nQ.T, d2 ); }
-  FE_FENCE();
+  nQp.YpX = c.YpX; nQp.YmX = c.YmX; nQp.T2d = c.T2d;
   ge_p3 P;
   ge_dbl( P, nQ, true ); ge_to_cached( c, P ); vtab_store( vtab, cap, t, 2, c );
 #pragma unroll 1

@@ -145,9 +145,9 @@ int fd_ed25519_verify_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx,
 /* Pipelined device-resident verify (throughput form of the entry above).
    Each call enqueues ONE launch that runs three phases of three batches:
    phase A of this batch (descriptor and S checks, SHA-512, lattice split,
-   w, decode + small-order check + table of A), phase B of the batch of the
-   previous call (decode + small-order check + table of R, the check-order
-   code, the top windows of the scalar-multiplication chain) and phase C of
+   w), phase B of the batch of the previous call (decode + small-order check
+   + table of A and of R, the check-order code, the top windows of the
+   scalar-multiplication chain) and phase C of
    the batch of the call before that (the rest of the chain, [w]B, the
    compare), which writes THAT batch's codes into its d_out.  So the codes of
    batch i are final once call i+2 (or fd_ed25519_gpu_pipe_flush_dev) has

@@ -5,10 +5,11 @@ Reads the amdhsa kernel metadata the assembler embeds (firedancer_amd/build/prod
 kern.opt.s, the exact code the library ships) and derives, per kernel, the
 occupancy limits on gfx950: 512 VGPRs per lane per SIMD (unified arch + acc file,
 allocation granule 8), 160 KB of LDS per CU, at most 8 waves per SIMD.  With the
-SQ counters of profiles/r01/pmc_sq.json it adds the achieved mean waves per SIMD
+SQ counters of profiles/r02/pmc_sq.json it adds the achieved mean waves per SIMD
 of the profiled verify launch (SQ_WAVE_CYCLES counts quad-cycles).
 
-  python3 tools/kernel_resources.py [out.json]
+  KR_ASM=<kern.opt.s> python3 tools/kernel_resources.py [out.json]   (default asm: the prod build,
+                                                                   default out: profiles/r02/kernel_resources.json)
 """
 import json
 import os
@@ -47,12 +48,14 @@ def limits(k):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r01", "kernel_resources.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r02", "kernel_resources.json")
+    if not out.endswith(".json"):
+        sys.exit("kernel_resources.py: the argument is the OUTPUT .json (the asm comes from KR_ASM or the prod build)")
     rep = {"source": os.path.relpath(ASM, REPO), "model": "gfx950: 512 VGPRs/SIMD lane, granule 8; "
            "160 KB LDS/CU; 8 waves/SIMD; 4 SIMDs/CU; 256 CUs", "kernels": {}}
     for k in metadata(ASM):
         rep["kernels"][k[".name"]] = limits(k)
-    pmc = os.path.join(REPO, "profiles", "r01", "pmc_sq.json")
+    pmc = os.path.join(REPO, "profiles", "r02", "pmc_sq.json")
     if os.path.exists(pmc):
         p = json.load(open(pmc))
         cyc = p["dur_ns"] * 1e-9 * p["effective_clock_ghz"] * 1e9
@@ -60,7 +63,7 @@ def main():
             "kernel": p["kernel"], "grid": p["grid"], "dur_ns": p["dur_ns"],
             "mean_waves_per_simd": 4.0 * p["SQ_WAVE_CYCLES"] / (cyc * SIMDS_PER_CU * CUS),
             "note": "SQ_WAVE_CYCLES (quad-cycles x4) / (launch cycles at the GRBM clock x 1,024 SIMDs); "
-                    "config 2 = one chain wave per SIMD, the pair kernel's second wave exits after [w]B",
+                    "config 2 pipelined = three waves per SIMD (phases A, B, C of three batches)",
         }
     json.dump(rep, open(out, "w"), indent=1)
     print(json.dumps(rep, indent=1))
