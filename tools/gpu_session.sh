@@ -1,6 +1,9 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3h.log 2>&1 || { tail -20 gpurun_out/smoke_s3h.log; exit 1; }
-tail -1 gpurun_out/smoke_s3h.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s3j.log 2>&1 || { tail -40 gpurun_out/gpu_tests_s3j.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_s3j.log
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3j.log 2>&1 || { tail -20 gpurun_out/smoke_s3j.log; exit 1; }
+tail -1 gpurun_out/smoke_s3j.log
+AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_ainb.so tools/bin/lib_new.so 2>&1 | grep -v amdgpu.ids | tee gpurun_out/ab_pipe_s3j.log
 bash tools/profile.sh r02s3
 bash tools/profile_configs.sh r02s3
