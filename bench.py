@@ -285,10 +285,17 @@ def main():
     d_outs = [d_out, torch.zeros(n, dtype=torch.int8, device=dev)]
     nstep = [0]
 
+    # a pipelined step over more than one wave per SIMD (config 3) is a run of
+    # pipe launches over chunks of pair_max descriptors (each launch one chunk
+    # of work, three chunks in flight across launches and across steps)
+    chunks = [(o, min(pair_max, n - o)) for o in range(0, n, pair_max)]
+
     def step():
-        if pipe:   # batch i's codes land in d_outs[i % 2] when launch i+2 completes
-            g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, d_outs[nstep[0] & 1].data_ptr(),
-                       stream=stream.cuda_stream)
+        if pipe:   # step i's codes land in d_outs[i % 2] once the launches two chunks later complete
+            out = d_outs[nstep[0] & 1]
+            for o, c in chunks:
+                g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr() + 16 * o, c, out.data_ptr() + o,
+                           stream=stream.cuda_stream)
             nstep[0] += 1
             return
         g.verify_batch_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, d_out.data_ptr(),

@@ -166,6 +166,22 @@ struct fparse_args {
 #define FD_KERN_FEMIT    "fd_frag_emit_kernel"
 #define FD_KERN_FFOLD    "fd_frag_fold_kernel"
 #define FD_KERN_PIPE     "fd_ed25519_verify_pipe_kernel"
+#define FD_KERN_LSORT    "fd_len_sort_kernel"
+
+/* SHA-block bucketing of one-shot launches above one wave per SIMD
+   (fd_len_sort_kernel): inside each segment of FD_LEN_SEG descriptors,
+   descriptor i goes to bucket min( blocks( 64 + msg_sz ), FD_LEN_NB-1 ),
+   blocks( n ) = (n + 17 + 127)/128, and the verify kernel takes the
+   descriptors in that order (list form), so a wave's lanes hash messages
+   of the same block count (a wave runs the SHA-512 loop for its longest
+   message). */
+#define FD_LEN_NB         16
+#define FD_LEN_SEG        8192
+struct len_args {
+  fd_ed25519_desc_t const * desc;
+  uint64_t                  n;
+  uint32_t *                idx;      /* n: descriptor indices, bucket order per segment */
+};
 
 /* Seeded key hash shared by the host (slot assignment) and the device
    (lookup): splitmix64 of the key's first 8 bytes xor seed. */

@@ -1291,6 +1291,41 @@ fd_ed25519_kcache_part_kernel( kpart_args a ) {
   if( miss ) { uint32_t o = base_m + (uint32_t)__popcll( bm & below ); a.miss_idx[ o ] = (uint32_t)i; }
 }
 
+/* ------------------------------------------------------------------ length buckets */
+
+__device__ __forceinline__ uint32_t len_bucket( fd_ed25519_desc_t const & d ) {
+  uint32_t b = (64u + (uint32_t)d.msg_sz + 17u + 127u) >> 7;
+  return min( b, (uint32_t)FD_LEN_NB - 1u );
+}
+
+/* Descriptor order by SHA-512 block count inside segments of FD_LEN_SEG
+   consecutive descriptors (one 1024-thread workgroup per segment, counting
+   sort in LDS): waves then hash messages of one block count, and a wave's
+   lanes still read arena bytes from one segment (a global sort scattered
+   them over the whole arena: the message loads then missed the TLB and the
+   1M-signature launch took 1.9x as long). */
+extern "C" __global__ void __launch_bounds__( 1024 )
+fd_len_sort_kernel( len_args a ) {
+  __shared__ uint32_t h[ FD_LEN_NB ], cur[ FD_LEN_NB ];
+  uint64_t lo = (uint64_t)blockIdx.x * FD_LEN_SEG;
+  if( lo >= a.n ) return;
+  uint32_t m = (uint32_t)min( (uint64_t)FD_LEN_SEG, a.n - lo );
+  uint32_t tid = threadIdx.x;
+  if( tid < FD_LEN_NB ) h[ tid ] = 0u;
+  __syncthreads();
+  for( uint32_t j=tid; j<m; j+=1024u ) atomicAdd( &h[ len_bucket( a.desc[ lo + j ] ) ], 1u );
+  __syncthreads();
+  if( tid == 0u ) {
+    uint32_t c = 0u;
+    for( int k=0; k<FD_LEN_NB; k++ ) { cur[k] = c; c += h[k]; }
+  }
+  __syncthreads();
+  for( uint32_t j=tid; j<m; j+=1024u ) {
+    uint32_t o = atomicAdd( &cur[ len_bucket( a.desc[ lo + j ] ) ], 1u );
+    a.idx[ lo + o ] = (uint32_t)(lo + j);
+  }
+}
+
 /* Key-table entry j (digit d != 0: entry |d|; d == 0: the identity record
    after the slots) of position p. */
 __device__ __forceinline__ void ktab_fetch( uint32_t w[ 32 ], uint32_t const * ktab, uint64_t kcap, uint64_t slot,

@@ -1,9 +1,7 @@
 set -e
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s3j.log 2>&1 || { tail -40 gpurun_out/gpu_tests_s3j.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_s3j.log
-timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3j.log 2>&1 || { tail -20 gpurun_out/smoke_s3j.log; exit 1; }
-tail -1 gpurun_out/smoke_s3j.log
-AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_ainb.so tools/bin/lib_new.so 2>&1 | grep -v amdgpu.ids | tee gpurun_out/ab_pipe_s3j.log
-bash tools/profile.sh r02s3
-bash tools/profile_configs.sh r02s3
+mkdir -p gpurun_out/ls
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+for V in 1 0; do
+  FD_ED25519_GPU_LENSORT=$V timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAVES SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/ls/v$V -o pmc -- python3 bench.py --config 3 --steps 3 --warmup 1 --no-cpu --pipeline 0 > /dev/null 2> gpurun_out/ls/v$V.err
+  python3 tools/pmc_summary.py gpurun_out/ls/v$V/pmc_counter_collection.csv mid
+done
