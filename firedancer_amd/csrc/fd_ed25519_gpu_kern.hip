@@ -533,7 +533,11 @@ __device__ __forceinline__ void vtab_fetch_lds( uint4 * buf, uint32_t const * vt
 /* Comb-table entry |d| of position k into buf[8][64]. */
 __device__ __forceinline__ void ctab_fetch_lds( uint4 * buf, uint32_t const * ctab, int k, int d ) {
   uint32_t e = (uint32_t)(d < 0 ? -d : d);
+#ifdef FD_DIAG_BIGCOMB   /* diagnostic (wrong results): the reads of a 23-bit comb table (11 x 2^22 entries, 5.9 GB) */
+  uint4 const * p = (uint4 const *)(ctab + ((uint64_t)k * 4194305u + ((e * 131u + (uint32_t)k * 977u) & 4194303u)) * FD_CTAB_STRIDE);
+#else
   uint4 const * p = (uint4 const *)(ctab + ((uint64_t)k * FD_CTAB_N + e) * FD_CTAB_STRIDE);
+#endif
 #pragma unroll
   for( int j=0; j<8; j++ ) __builtin_amdgcn_global_load_lds( (void const *)(p + j), (lds_void_t *)(buf + 64*j), 16, 0, 0 );
 }
