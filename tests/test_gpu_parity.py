@@ -258,7 +258,17 @@ def test_pair_and_single_lane_kernels_agree(gpu):
     finally:
         del os.environ["FD_ED25519_GPU_PAIR"]
     try:
+        # the single-lane kernel takes its descriptors in SHA-block-count order
+        # (fd_len_sort_kernel, list form): the golden records span 0..~1.2K-byte
+        # messages, so every bucket and both code flavours go through that path
         assert np.array_equal(single.verify_batch(arena, sz, desc), exp)
+        single.set_codes(fa.CODES_REF)
+        exp_ref = np.array([r["code_ref"] for r in recs], dtype=np.int8)
+        assert np.array_equal(single.verify_batch(arena, sz, desc), exp_ref)
+        # and twice over in a different order (codes land at the descriptor's index)
+        perm = np.random.default_rng(3).permutation(np.concatenate([np.arange(len(desc)), np.arange(len(desc))]))
+        single.set_codes(fa.CODES_AVX512)
+        assert np.array_equal(single.verify_batch(arena, sz, desc[perm].copy()), exp[perm])
     finally:
         single.close()
     assert np.array_equal(gpu.verify_batch(arena, sz, desc), exp)
