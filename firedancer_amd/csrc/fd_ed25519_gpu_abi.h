@@ -13,10 +13,12 @@
 #ifndef FD_VERIFY_WAVES_PER_EU
 #define FD_VERIFY_WAVES_PER_EU 2       /* -> <= 256 VGPR+AGPR per lane                */
 #endif
-#define FD_CTAB_POS       16           /* signed 16-bit windows of w < 2^253           */
-#define FD_CTAB_N         32769        /* entries [0..2^15](2^(16 k) B) per position   */
+#define FD_CTAB_BITS      23           /* signed 23-bit windows of w < l < 2^253 (fd_scalar_dev.h comb_digit) */
+#define FD_CTAB_POS       11           /* 11 x 23 = 253                                */
+#define FD_CTAB_HALF      (1u << 22)
+#define FD_CTAB_N         (FD_CTAB_HALF + 1u)   /* entries [0..2^22](2^(23 k) B) per position */
 #define FD_CTAB_STRIDE    32           /* u32 per entry: 3 x 10 limbs + pad (128 B)    */
-#define FD_CTAB_WORDS     ((uint64_t)FD_CTAB_POS * FD_CTAB_N * FD_CTAB_STRIDE)   /* 67 MB */
+#define FD_CTAB_WORDS     ((uint64_t)FD_CTAB_POS * FD_CTAB_N * FD_CTAB_STRIDE)   /* 5.9 GB */
 #define FD_VTAB_N         9            /* [0..8](-Q), Q = A or R                      */
 #define FD_VTAB_WORDS     40           /* u32 per entry (4 fe)                        */
 /* Word of limb j of field f (0: Y+X, 1: Y-X, 2: 2dT, 3: 2Z) in a variable-
@@ -45,9 +47,9 @@
 /* LDS digit rows ([row][slot] bytes) */
 #define FD_ROW_U          0            /* signed 4-bit digits of u (sign folded in)   */
 #define FD_ROW_V          64           /* signed 4-bit digits of v                    */
-#define FD_ROW_W          128          /* signed 16-bit digits of w = v S mod l: 16 x (lo, hi) rows */
-#define FD_ROW_NW         160          /* lane 0 of each wave: the wave's window count */
-#define FD_ROWS           161
+#define FD_ROW_W          128          /* signed 23-bit comb digits of w = v S mod l: 11 x 3 byte rows (LE, two's complement) */
+#define FD_ROW_NW         161          /* lane 0 of each wave: the wave's window count */
+#define FD_ROWS           162
 
 
 struct verify_args {
@@ -87,7 +89,7 @@ struct verify_args {
 #define FD_PH_R           0            /* R's encoding, 8 words                        */
 #define FD_PH_YU          8            /* u + 8 (16^0 + ... + 16^(nw-2)), 8 words      */
 #define FD_PH_YV          16           /* v + the same bias, 8 words                   */
-#define FD_PH_YW          24           /* w + 2^15 (2^0 + ... + 2^224), 8 words        */
+#define FD_PH_YW          24           /* comb_bias(w) = w + 2^22 (2^0 + 2^23 + ... + 2^207)   */
 #define FD_PH_A           32           /* A's encoding, 8 words                        */
 #define FD_PH_WORDS       40
 #define FD_PACC_WORDS     40           /* X, Y, Z, T                                   */
@@ -156,6 +158,7 @@ struct fparse_args {
 #define FD_KERN_VERIFY   "fd_ed25519_verify_kernel"
 #define FD_KERN_VPAIR    "fd_ed25519_verify_pair_kernel"
 #define FD_KERN_CTAB     "fd_ed25519_ctab_init"
+#define FD_KERN_CBASE    "fd_ed25519_ctab_base"
 #define FD_KERN_LATTEST  "fd_ed25519_lattice_test_kernel"
 #define FD_KERN_SHA512   "fd_sha512_batch_kernel"
 #define FD_KERN_KBUILD   "fd_ed25519_ktab_build_kernel"

@@ -9,8 +9,8 @@
      (fd_lattice_dev.h) -> decode A and R (sqrt-ratio ladder), small-order
      checks -> per-lane tables [0..8](-A), [0..8](-R) in HBM ->
      Q = [u](-A) + [v](-R) in ONE ~130-doubling Straus chain, then + [w]B
-     as 16 mixed additions from the fixed-base comb table
-     [0..2^15](2^(16 k) B), k < 16 (67 MB in HBM, built once per device)
+     as 11 mixed additions from the fixed-base comb table
+     [0..2^22](2^(23 k) B), k < 11 (5.9 GB in HBM, built once per context)
      -> Q == O.
    Semantics follow fd_ed25519_verify (src/ballet/ed25519/fd_ed25519_user.c:
    134-229) with the FD_HAS_AVX512 error mapping (SURVEY.md §8(a) A-spec). */
@@ -62,31 +62,46 @@ __device__ void ge_affine_precomp( ge_precomp & q, ge_p3 & p ) {
   p.X = x; p.Y = y; fe_set1( p.Z ); p.T = xy;
 }
 
-/* Device init of the fixed-base comb table: thread g = k*FD_CTAB_N + j
-   computes [j](2^(16 k) B) (16 k doublings of B, then a 16-bit
-   double-and-add) and stores its affine precomputed form (Y+X, Y-X, 2dXY)
-   at ctab[g*FD_CTAB_STRIDE ...].  B decoded from its standard encoding
-   (y = 4/5, x even).  Runs once per device at context creation. */
-extern "C" __global__ void __launch_bounds__( 256 ) fd_ed25519_ctab_init( uint32_t * ctab ) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if( g >= (uint32_t)(FD_CTAB_POS*FD_CTAB_N) ) return;
-  uint32_t k = g / FD_CTAB_N, j = g % FD_CTAB_N;
+/* Bases of the fixed-base comb table: thread k < FD_CTAB_POS computes
+   B_k = [2^(23 k)] B (23 k doublings of B, decoded from its standard
+   encoding: y = 4/5, x even) and stores its affine precomputed form (Y+X,
+   Y-X, 2dXY; 30 words) at cbase[30 k].  Runs once per device at context
+   creation, before fd_ed25519_ctab_init. */
+extern "C" __global__ void __launch_bounds__( 64 ) fd_ed25519_ctab_base( uint32_t * cbase ) {
+  uint32_t k = threadIdx.x;
+  if( k >= (uint32_t)FD_CTAB_POS ) return;
   uint32_t benc[ 8 ];
   benc[0] = 0x66666658u;
 #pragma unroll
   for( int i=1; i<8; i++ ) benc[i] = 0x66666666u;
   ge_p3 B; ge_decode( B, benc, true );
 #pragma unroll 1
-  for( uint32_t i=0; i<16u*k; i++ ) ge_dbl( B, B, false );
+  for( uint32_t i=0; i<(uint32_t)FD_CTAB_BITS*k; i++ ) ge_dbl( B, B, false );
   ge_precomp Bp; ge_affine_precomp( Bp, B );
+#pragma unroll
+  for( int i=0; i<10; i++ ) { cbase[30*k + i] = Bp.YpX.v[i]; cbase[30*k + 10 + i] = Bp.YmX.v[i]; cbase[30*k + 20 + i] = Bp.T2d.v[i]; }
+}
+
+/* The fixed-base comb table: thread g = k FD_CTAB_N + j computes [j] B_k
+   (23-bit double-and-add from the affine base, j <= 2^22) and stores its
+   affine precomputed form (Y+X, Y-X, 2dXY) at ctab[g FD_CTAB_STRIDE ...]
+   (entry 0: the identity, Y+X = Y-X = 1, 2dXY = 0).  11 x (2^22+1)
+   entries, 5.9 GB; runs once per device at context creation (~0.1 s). */
+extern "C" __global__ void __launch_bounds__( 256 ) fd_ed25519_ctab_init( uint32_t * ctab, uint32_t const * cbase ) {
+  uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( g >= (uint64_t)FD_CTAB_POS * FD_CTAB_N ) return;
+  uint32_t k = (uint32_t)(g / FD_CTAB_N), j = (uint32_t)(g % FD_CTAB_N);
+  ge_precomp Bp;
+#pragma unroll
+  for( int i=0; i<10; i++ ) { Bp.YpX.v[i] = cbase[30*k + i]; Bp.YmX.v[i] = cbase[30*k + 10 + i]; Bp.T2d.v[i] = cbase[30*k + 20 + i]; }
   ge_p3 acc; ge_identity( acc );
 #pragma unroll 1
-  for( int bit=15; bit>=0; bit-- ) {
+  for( int bit=FD_CTAB_BITS-1; bit>=0; bit-- ) {
     ge_dbl( acc, acc, true );
     if( (j >> bit) & 1u ) ge_madd( acc, acc, Bp, true );
   }
   ge_precomp o; ge_affine_precomp( o, acc );
-  uint4 * e = (uint4 *)(ctab + (uint64_t)g * FD_CTAB_STRIDE);
+  uint4 * e = (uint4 *)(ctab + g * FD_CTAB_STRIDE);
   uint32_t w[ 32 ];
 #pragma unroll
   for( int i=0; i<10; i++ ) { w[i] = o.YpX.v[i]; w[10+i] = o.YmX.v[i]; w[20+i] = o.T2d.v[i]; }
@@ -246,10 +261,10 @@ __device__ __forceinline__ void vtab_finish( ge_cached & c, uint32_t const w[ 40
   }
 }
 
-/* Comb-table entry |d| of position k (signed 16-bit digit d): loads issued
+/* Comb-table entry |d| of position k (signed 23-bit digit d): loads issued
    here, sign applied by ctab_finish at the use point. */
 __device__ __forceinline__ void ctab_fetch( uint32_t w[ 32 ], uint32_t const * ctab, int k, int d ) {
-  uint32_t e = (uint32_t)(d < 0 ? -d : d);
+  uint32_t e = min( (uint32_t)(d < 0 ? -d : d), FD_CTAB_HALF );    /* |d| <= 2^22 by construction; never past the table */
   uint4 const * p = (uint4 const *)(ctab + ((uint64_t)k * FD_CTAB_N + e) * FD_CTAB_STRIDE);
 #pragma unroll
   for( int j=0; j<8; j++ ) { uint4 v = p[j]; w[4*j] = v.x; w[4*j+1] = v.y; w[4*j+2] = v.z; w[4*j+3] = v.w; }
@@ -270,15 +285,16 @@ __device__ __forceinline__ void ctab_finish( ge_precomp & q, uint32_t const w[ 3
 }
 
 __device__ __forceinline__ int wdig( uint8_t const * dig, int k ) {
-  uint32_t lo = dig[ (FD_ROW_W + 2*k)*FD_VERIFY_BLOCK ], hi = dig[ (FD_ROW_W + 2*k + 1)*FD_VERIFY_BLOCK ];
-  return (int)(int16_t)(uint16_t)(lo | (hi << 8));
+  uint32_t b0 = dig[ (FD_ROW_W + 3*k)*FD_VERIFY_BLOCK ], b1 = dig[ (FD_ROW_W + 3*k + 1)*FD_VERIFY_BLOCK ];
+  uint32_t b2 = dig[ (FD_ROW_W + 3*k + 2)*FD_VERIFY_BLOCK ];
+  return ((int)((b0 | (b1 << 8) | (b2 << 16)) << 8)) >> 8;      /* 24-bit two's complement */
 }
 
 /* acc = [u](-A) + [v](-R) over nw 4-bit windows (wave-uniform; one shared
-   doubling chain -- Straus), then + [w]B as 16 mixed additions of comb-table
-   entries (no doublings: entry k already carries its 2^(16 k)).  u / v
+   doubling chain -- Straus), then + [w]B as 11 mixed additions of comb-table
+   entries (no doublings: entry k already carries its 2^(23 k)).  u / v
    digits from LDS rows (biased by 8, sign of u folded in), w digits signed
-   16-bit.  Table entries are fetched one step ahead: A's for the next window
+   23-bit (three byte rows each).  Table entries are fetched one step ahead: A's for the next window
    before the doublings, R's before A's addition, the first comb entry during
    the last window. */
 template<bool COMB>
@@ -325,7 +341,7 @@ __device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, ui
   }
 }
 
-/* c = [w]B alone: the 16 comb-table additions of dsm_loop from the identity
+/* c = [w]B alone: the 11 comb-table additions of dsm_loop from the identity
    (the pair kernel's second wave computes it beside the chain). */
 __device__ __forceinline__ void comb_only( ge_p3 & c, uint8_t const * dig, uint32_t const * ctab ) {
   ge_identity( c );
@@ -425,16 +441,15 @@ __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, uint64_t str
                          , _st
 #endif
                          );
-    /* signed 16-bit windows: d_k in [-2^15, 2^15), the top one (w < 2^253)
-       keeps its carry: d_15 <= 2^13 */
-    int c = 0;
+    /* signed 23-bit comb digits (fd_scalar_dev.h comb_digit), three bytes each */
+    uint32_t yw[ 8 ];
+    comb_bias( yw, w );
 #pragma unroll
     for( int k=0; k<FD_CTAB_POS; k++ ) {
-      int dd = (int)((w[k>>1] >> (16*(k&1))) & 0xffffu) + c;
-      c = dd >= 32768 && k < FD_CTAB_POS-1;
-      dd -= c << 16;
-      drow[ (uint64_t)(FD_ROW_W + 2*k    )*stride ] = (uint8_t)(dd & 255);
-      drow[ (uint64_t)(FD_ROW_W + 2*k + 1)*stride ] = (uint8_t)((dd >> 8) & 255);
+      int dd = comb_digit( yw, k );
+      drow[ (uint64_t)(FD_ROW_W + 3*k    )*stride ] = (uint8_t)(dd & 255);
+      drow[ (uint64_t)(FD_ROW_W + 3*k + 1)*stride ] = (uint8_t)((dd >> 8) & 255);
+      drow[ (uint64_t)(FD_ROW_W + 3*k + 2)*stride ] = (uint8_t)((dd >> 16) & 255);
     }
   }
   int nw = wave_windows( nbits );
@@ -532,12 +547,8 @@ __device__ __forceinline__ void vtab_fetch_lds( uint4 * buf, uint32_t const * vt
 
 /* Comb-table entry |d| of position k into buf[8][64]. */
 __device__ __forceinline__ void ctab_fetch_lds( uint4 * buf, uint32_t const * ctab, int k, int d ) {
-  uint32_t e = (uint32_t)(d < 0 ? -d : d);
-#ifdef FD_DIAG_BIGCOMB   /* diagnostic (wrong results): the reads of a 23-bit comb table (11 x 2^22 entries, 5.9 GB) */
-  uint4 const * p = (uint4 const *)(ctab + ((uint64_t)k * 4194305u + ((e * 131u + (uint32_t)k * 977u) & 4194303u)) * FD_CTAB_STRIDE);
-#else
+  uint32_t e = min( (uint32_t)(d < 0 ? -d : d), FD_CTAB_HALF );
   uint4 const * p = (uint4 const *)(ctab + ((uint64_t)k * FD_CTAB_N + e) * FD_CTAB_STRIDE);
-#endif
 #pragma unroll
   for( int j=0; j<8; j++ ) __builtin_amdgcn_global_load_lds( (void const *)(p + j), (lds_void_t *)(buf + 64*j), 16, 0, 0 );
 }
@@ -611,13 +622,6 @@ __device__ __forceinline__ void ybias4( uint32_t y[ 8 ], uint32_t const x[ 8 ], 
   }
 }
 
-/* w + 2^15 (2^0 + 2^16 + ... + 2^224): the signed 16-bit comb digits as a
-   bias (digit k = half k - 2^15 for k < 15, the top one unbiased). */
-__device__ __forceinline__ void ybias16( uint32_t y[ 8 ], uint32_t const w[ 8 ] ) {
-  uint64_t c = 0;
-#pragma unroll
-  for( int j=0; j<8; j++ ) { c += (uint64_t)w[j] + (j < 7 ? 0x80008000u : 0x00008000u); y[j] = (uint32_t)c; c >>= 32; }
-}
 
 /* Windows hi-1 .. lo of the Straus chain acc = [u](-A) + [v](-R) (dsm_loop's
    order: four doublings unless it is the chain's first window, then A's and
@@ -666,14 +670,14 @@ __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t co
   }
 }
 
-/* acc += [w]B: the 16 comb-table additions, w's biased digits in yw.
+/* acc += [w]B: the 11 comb-table additions, w's biased digits in yw.
    (FD_DIAG_COMB_POS < FD_CTAB_POS: diagnostic build, wrong results, timing
    of fewer comb additions.) */
 #ifndef FD_DIAG_COMB_POS
 #define FD_DIAG_COMB_POS FD_CTAB_POS
 #endif
 __device__ __forceinline__ void comb_lds( ge_p3 & acc, uint4 * buf, uint32_t const * yw, int lane, uint32_t const * ctab ) {
-#define FD_WDIG( k ) ((int)((yw[ ((k) >> 1)*64 + lane ] >> (16*((k) & 1))) & 0xffffu) - ((k) < FD_CTAB_POS-1 ? 32768 : 0))
+#define FD_WDIG( k ) comb_digit_w( yw[ ((23*(k)) >> 5)*64 + lane ], ((23*(k)) >> 5) < 7 ? yw[ (((23*(k)) >> 5) + 1)*64 + lane ] : 0u, (k) )
   int d = FD_WDIG( 0 );
   ctab_fetch_lds( buf, ctab, 0, d );
 #pragma unroll 1
@@ -768,7 +772,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
     ybias4( t, v, nw );
 #pragma unroll
     for( int j=0; j<8; j++ ) y[ (8 + j)*64 + lane ] = t[j];
-    ybias16( t, w );
+    comb_bias( t, w );
 #pragma unroll
     for( int j=0; j<8; j++ ) y[ (16 + j)*64 + lane ] = t[j];
     nwin = nw;
@@ -838,7 +842,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
    has two waves per SIMD (the single-wave kernel issues one VALU op per ~4.9
    cycles per SIMD; two waves of the same code fill more of the issue slots;
    same code, so no extra instruction-cache footprint); role 1 leaves the
-   status of R in LDS, computes [w]B (the 16 comb additions) beside role 0's
+   status of R in LDS, computes [w]B (the 11 comb additions) beside role 0's
    chain and hands it over in LDS (cached form) at the second barrier; role 0
    runs the Straus chain and adds it.  Bit-identical results to
    fd_ed25519_verify_kernel (same functions, same order of checks).
@@ -908,7 +912,7 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
   }
   if( role ) s_stR[ tid ] = (uint8_t)stq;
   if( role ) {
-    /* [w]B beside role 0's chain (16 comb additions; w digits came before
+    /* [w]B beside role 0's chain (11 comb additions; w digits came before
        the first barrier) */
     ge_p3 c;
     ge_cached cc;
@@ -940,7 +944,7 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
      waves 4-7  (phase B), batch j-1: decode A, small-order A, A's table,
        decode R, small-order R, R's table, the check-order code, then the
        TOP kb windows of the Straus chain;
-     waves 0-3  (phase C), batch j-2: the remaining windows, the 16 comb
+     waves 0-3  (phase C), batch j-2: the remaining windows, the 11 comb
        additions of [w]B and the compare.
    Why: config 2 is one 64-signature wave per SIMD; a single wave issues a
    VALU instruction per ~4.6 cycles, the SIMD takes one per ~4.05 from
@@ -1038,7 +1042,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       ybias4( y, v, nw );
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YV + j)*cap ] = y[j];
-      ybias16( y, w );
+      comb_bias( y, w );
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YW + j)*cap ] = y[j];
 #pragma unroll
@@ -1423,20 +1427,22 @@ fd_ed25519_verify_cached_kernel( verify_args args ) {
       ge_madd( acc, acc, e, true );
       FE_FENCE();
     }
-    /* + [S]B from the fixed-base comb table (signed 16-bit windows of S) */
-    int cs = 0, ds;
-    {
-      int dd = (int)(ss[0] & 0xffffu); cs = dd >= 32768; ds = dd - (cs << 16);
-    }
+    /* + [S]B from the fixed-base comb table (signed 23-bit comb digits of
+       S < l, fd_scalar_dev.h; lanes that do not run have S = 0) */
+    uint32_t ys[ 8 ];
+    comb_bias( ys, ss );
+    int ds = comb_digit( ys, 0 );
     ctab_fetch( raw, args.ctab, 0, ds );
 #pragma unroll 1
     for( int q=0; q<FD_CTAB_POS; q++ ) {
       ge_precomp e;
       ctab_finish( e, raw, ds );
       if( q + 1 < FD_CTAB_POS ) {
-        int dd = (int)((ss[(q+1)>>1] >> (16*((q+1)&1))) & 0xffffu) + cs;
-        cs = dd >= 32768 && q + 1 < FD_CTAB_POS-1;
-        ds = dd - (cs << 16);
+        /* the next digit by shifting ys down 23 bits (no dynamic register index) */
+#pragma unroll
+        for( int j=0; j<7; j++ ) ys[j] = __builtin_amdgcn_alignbit( ys[j+1], ys[j], 23u );
+        ys[7] >>= 23;
+        ds = (int)(ys[0] & ((1u << 23) - 1u)) - (q + 1 < 10 ? (1 << 22) : 0);
         ctab_fetch( raw, args.ctab, q + 1, ds );
       }
       FE_FENCE();

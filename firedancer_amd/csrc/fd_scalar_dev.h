@@ -126,4 +126,29 @@ FD_SC_FN void sc_recode_w8( uint8_t out[ 32 ], uint32_t const s[ 8 ] ) {
   }
 }
 
+/* Signed radix-2^23 comb digits of w < l (the fixed-base comb table,
+   fd_ed25519_gpu_abi.h FD_CTAB_*): y = w + sum_{k<10} 2^22 2^(23 k) (the
+   recoding as a bias), then d_k = bits [23 k, 23 k + 23) of y minus 2^22
+   for k < 10 (in [-2^22, 2^22)) and d_10 = y >> 230 unbiased (in
+   [0, 2^22]: w < l = 2^252 + 2^124.4 and the bias is below 2^229 + 1, so
+   y < 2^252 + 2^230); sum_k d_k 2^(23 k) = w. */
+FD_SC_FN void comb_bias( uint32_t y[ 8 ], uint32_t const w[ 8 ] ) {
+  uint32_t const b[ 8 ] = { 0x400000u, 0x2000u, 0x8000010u, 0x40000u, 0x200u, 0x800001u, 0x4000u, 0x20u };
+  uint64_t c = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) { c += (uint64_t)w[j] + b[j]; y[j] = (uint32_t)c; c >>= 32; }
+}
+
+/* Digit k of a comb_bias'ed y (words lo = y[(23 k) >> 5], hi = the next word
+   or 0 past the top, r = (23 k) & 31). */
+FD_SC_FN int comb_digit_w( uint32_t lo, uint32_t hi, int k ) {
+  int r = (23*k) & 31;
+  uint32_t x = (uint32_t)((((uint64_t)hi << 32) | lo) >> r) & ((1u << 23) - 1u);
+  return (int)x - (k < 10 ? (1 << 22) : 0);
+}
+FD_SC_FN int comb_digit( uint32_t const y[ 8 ], int k ) {
+  int q = (23*k) >> 5;
+  return comb_digit_w( y[q], q < 7 ? y[q+1] : 0u, k );
+}
+
 #endif /* FD_SCALAR_DEV_H */

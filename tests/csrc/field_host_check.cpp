@@ -21,6 +21,17 @@ int  t_sc_lt_l( uint32_t const * s ) { return sc_lt_l( s ); }
 void t_recode4( uint8_t * o, uint32_t const * s ) { sc_recode_w4( o, s ); }
 void t_recode8( uint8_t * o, uint32_t const * s ) { sc_recode_w8( o, s ); }
 void t_sha_block( uint64_t * h, uint64_t * w ) { sha512_compress( h, w ); }
+void t_comb_digits( int * d, uint32_t const * w ) {
+  uint32_t y[ 8 ]; comb_bias( y, w );
+  for( int k=0; k<11; k++ ) d[k] = comb_digit( y, k );
+  /* the cached kernel's form: shift the biased scalar down 23 bits per digit */
+  for( int k=1; k<11; k++ ) {
+    for( int j=0; j<7; j++ ) y[j] = (uint32_t)((((uint64_t)y[j+1] << 32) | y[j]) >> 23);
+    y[7] >>= 23;
+    int dd = (int)(y[0] & ((1u << 23) - 1u)) - (k < 10 ? (1 << 22) : 0);
+    if( dd != d[k] ) d[k] = 0x7fffffff;      /* disagreement flag */
+  }
+}
 }
 #include "../../firedancer_amd/csrc/fd_lattice_dev.h"
 extern "C" {

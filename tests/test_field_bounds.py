@@ -204,3 +204,22 @@ def test_lattice_short_vector_host(lib):
 
 def val32(w):
     return sum(int(x) << (32 * i) for i, x in enumerate(w))
+
+
+def test_comb_digits(lib):
+    """The fixed-base comb's signed 23-bit digits (fd_scalar_dev.h comb_bias /
+    comb_digit, and the cached kernel's shifting form): sum d_k 2^(23 k) = w,
+    |d_k| <= 2^22 for k < 10 and 0 <= d_10 <= 2^22 (the table's 2^22 + 1
+    entries per position), for random w < l and the edges."""
+    rng = random.Random(23)
+    ws = [rng.randrange(LL) for _ in range(20000)] + [0, 1, LL - 1, LL - 2, 2**252 - 1, 2**252, 2**230,
+                                                     2**230 - 1, 2**22, 2**22 - 1, 2**23 - 1, 2**23]
+    ws += [sum(rng.choice([0, 2**22 - 1, 2**22, 2**23 - 1]) << (23 * k) for k in range(10)) % LL for _ in range(2000)]
+    ws += [(LL - 1) - sum(rng.choice([0, 1, 2**22]) << (23 * k) for k in range(10)) for _ in range(2000)]
+    d = (ctypes.c_int * 11)()
+    for w in ws:
+        lib.t_comb_digits(d, arr([(w >> (32 * j)) & 0xffffffff for j in range(8)]))
+        dd = list(d)
+        assert 0x7fffffff not in dd, w
+        assert sum(x << (23 * k) for k, x in enumerate(dd)) == w, w
+        assert all(-2**22 <= x < 2**22 for x in dd[:10]) and 0 <= dd[10] <= 2**22, (w, dd)
