@@ -1,15 +1,8 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 200 python3 -c "
-import time, ctypes, torch
-torch.cuda.init()
-for L in ('tools/bin/lib_new.so', 'tools/bin/lib_comb23.so', 'tools/bin/lib_new.so', 'tools/bin/lib_comb23.so'):
-    lib = ctypes.CDLL(L); lib.fd_ed25519_gpu_new.restype = ctypes.c_void_p; lib.fd_ed25519_gpu_new.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
-    lib.fd_ed25519_gpu_delete.argtypes = [ctypes.c_void_p]
-    t = time.perf_counter(); c = lib.fd_ed25519_gpu_new(1, 65536); dt = time.perf_counter() - t; assert c; lib.fd_ed25519_gpu_delete(c)
-    print(L, 'context creation %.3f s' % dt, flush=True)
-" 2>&1 | grep -v amdgpu.ids | tee gpurun_out/ctx_time_s3u.log
-for r in 1 2 3; do
-AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_new.so tools/bin/lib_comb23.so 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_comb23_s3u.log
-AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_comb23.so tools/bin/lib_new.so 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_comb23_s3u.log
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s3v.log 2>&1 || { tail -40 gpurun_out/gpu_tests_s3v.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_s3v.log
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3v.log 2>&1 || { tail -20 gpurun_out/smoke_s3v.log; exit 1; }
+tail -1 gpurun_out/smoke_s3v.log
+bash tools/profile.sh r02s3v
+bash tools/profile_configs.sh r02s3v
