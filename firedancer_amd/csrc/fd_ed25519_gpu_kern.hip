@@ -29,6 +29,7 @@
    build compiles none of it. */
 #ifdef FD_PHASE_STAMPS
 #define FD_NSTAMP 8
+#define FD_TL_BASE 8      /* pipe-kernel timeline: 4 u64 per wave after the sums */
 #define STAMP( i ) do { FE_FENCE(); if( _st ) _st[ i ] = __builtin_amdgcn_s_memtime(); FE_FENCE(); } while( 0 )
 #else
 #define STAMP( i ) do {} while( 0 )
@@ -996,6 +997,18 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   }
 #ifdef FD_PHASE_STAMPS
   uint64_t t0 = __builtin_amdgcn_s_memtime();
+  uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+  /* per-wave timeline of the launch (the last one before the context closes):
+     start / end on the constant-rate clock, HW_ID and XCC_ID, cycles */
+#define FD_TL_STAMP() do {                                                                              \
+    if( args.stamps && lane == 0 ) {                                                                    \
+      unsigned long long * tl = args.stamps + FD_TL_BASE + ((uint64_t)blockIdx.x * 12u + (uint64_t)(role*4 + wv)) * 4u; \
+      uint64_t rt1 = __builtin_amdgcn_s_memrealtime();                                                  \
+      uint32_t hw = __builtin_amdgcn_s_getreg( (31 << 11) | 4 ), xcc = __builtin_amdgcn_s_getreg( (15 << 11) | 20 ); \
+      tl[0] = rt0; tl[1] = rt1; tl[2] = ((uint64_t)xcc << 32) | hw; tl[3] = __builtin_amdgcn_s_memtime() - t0; \
+    } } while( 0 )
+#else
+#define FD_TL_STAMP() do {} while( 0 )
 #endif
 
   if( role == 2 ) {
@@ -1056,6 +1069,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #ifdef FD_PHASE_STAMPS
     if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[5], 1ull ); }
 #endif
+    FD_TL_STAMP();
     return;
   }
 
@@ -1146,6 +1160,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #ifdef FD_PHASE_STAMPS
   if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[phb ? 1 : 0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[phb ? 6 : 7], 1ull ); }
 #endif
+  FD_TL_STAMP();
 }
 
 /* ------------------------------------------------------------------ SHA-512 batch */

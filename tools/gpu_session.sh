@@ -1,8 +1,8 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s3v.log 2>&1 || { tail -40 gpurun_out/gpu_tests_s3v.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_s3v.log
-timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3v.log 2>&1 || { tail -20 gpurun_out/smoke_s3v.log; exit 1; }
-tail -1 gpurun_out/smoke_s3v.log
-bash tools/profile.sh r02s3v
-bash tools/profile_configs.sh r02s3v
+timeout -k 10 300 python -u -m pytest tests/test_pipe.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pipe_multi_tests.log 2>&1 || { tail -40 gpurun_out/pipe_multi_tests.log; exit 1; }
+tail -1 gpurun_out/pipe_multi_tests.log
+for md in 0 0x201 0x301 0x101; do
+echo "mode $md" | tee -a gpurun_out/quick_multi_s3z.log
+FD_ED25519_GPU_PIPE_MODE=$md timeout -k 10 200 python3 tools/quick_multi.py 65536 96 3 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/quick_multi_s3z.log
+done
