@@ -91,7 +91,8 @@ struct verify_args {
 #define FD_PH_YV          16           /* v + the same bias, 8 words                   */
 #define FD_PH_YW          24           /* comb_bias(w) = w + 2^22 (2^0 + 2^23 + ... + 2^207)   */
 #define FD_PH_A           32           /* A's encoding, 8 words                        */
-#define FD_PH_WORDS       40
+#define FD_PH_IDX         40           /* the descriptor index the slot verifies        */
+#define FD_PH_WORDS       41
 #define FD_PACC_WORDS     40           /* X, Y, Z, T                                   */
 #define FD_PIPE_SETS      3
 struct pipe_args {
@@ -99,6 +100,7 @@ struct pipe_args {
   uint64_t                  sig_cap;    /* slots per set */
   uint64_t                  kb;         /* windows of the chain in phase B (>= 1) */
   uint64_t                  prio;       /* wave priority of phase C / B / A: bits 0-1 / 2-3 / 4-5 */
+  uint64_t                  lsort;      /* phase A: length order inside full workgroups */
   uint64_t                  set_a, set_b, set_c;
   uint32_t *                hand_a;     /* phase A writes */
   uint8_t *                 st_a;

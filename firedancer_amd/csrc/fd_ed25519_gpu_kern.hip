@@ -965,6 +965,55 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
    of in 40 VGPRs: 168 VGPRs are the budget of three waves per SIMD.  Same
    device functions and check order as fd_ed25519_verify_kernel:
    bit-identical codes. */
+/* SHA-512 block count of R || A || M (the length-order key, clamped). */
+__device__ __forceinline__ uint32_t len_bucket( fd_ed25519_desc_t const & d ) {
+  uint32_t b = (64u + (uint32_t)d.msg_sz + 17u + 127u) >> 7;
+  return min( b, (uint32_t)FD_LEN_NB - 1u );
+}
+
+/* Phase A's descriptor order inside a full workgroup (256 descriptors): a
+   wave runs the SHA-512 loop for its longest message, so the four phase-A
+   waves of a workgroup take the 256 descriptors ordered by block count (a
+   counting sort over the four waves' ballots, through LDS) instead of 64
+   consecutive ones each.  With Uniform{0..1232}-B messages a wave's longest
+   is then the 1/4..4/4 quantile of 256 instead of the maximum every time.
+   Returns the descriptor index (within the workgroup) slot t = w*64 + lane
+   takes.  The four waves wait for each other on LDS counters zeroed by the
+   workgroup's barrier at kernel start (bounded waits: all four are resident
+   in the workgroup, so they arrive). */
+__device__ __forceinline__ uint32_t pipe_len_order( uint32_t key, int w, int lane, uint32_t * wh, uint32_t * perm,
+                                                    uint32_t * flag ) {
+  uint64_t below = (1ull << lane) - 1ull;
+  uint32_t mine = 0, rank = 0;
+#pragma unroll 1
+  for( uint32_t b=0; b<(uint32_t)FD_LEN_NB; b++ ) {
+    uint64_t m = __ballot( key == b );
+    if( lane == (int)b ) mine = (uint32_t)__popcll( m );
+    if( key == b ) rank = (uint32_t)__popcll( m & below );
+  }
+  if( lane < FD_LEN_NB ) wh[ w*FD_LEN_NB + lane ] = mine;
+  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "workgroup" );
+  if( lane == 0 ) __hip_atomic_fetch_add( &flag[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP );
+  for( uint32_t i=0; i<(1u<<20) && __hip_atomic_load( &flag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u; i++ )
+    __builtin_amdgcn_s_sleep( 1 );
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "workgroup" );
+  uint32_t pos = rank;
+#pragma unroll 1
+  for( uint32_t b=0; b<(uint32_t)FD_LEN_NB; b++ ) {
+    uint32_t c0 = wh[ b ], c1 = wh[ FD_LEN_NB + b ], c2 = wh[ 2*FD_LEN_NB + b ], c3 = wh[ 3*FD_LEN_NB + b ];
+    uint32_t tot = c0 + c1 + c2 + c3;
+    uint32_t pre = (w > 0 ? c0 : 0u) + (w > 1 ? c1 : 0u) + (w > 2 ? c2 : 0u);
+    pos += b < key ? tot : (b == key ? pre : 0u);
+  }
+  perm[ pos ] = (uint32_t)(w*64 + lane);
+  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "workgroup" );
+  if( lane == 0 ) __hip_atomic_fetch_add( &flag[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP );
+  for( uint32_t i=0; i<(1u<<20) && __hip_atomic_load( &flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u; i++ )
+    __builtin_amdgcn_s_sleep( 1 );
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "workgroup" );
+  return perm[ w*64 + lane ];
+}
+
 #define FD_PIPE_ST_VALID  0x80      /* phase A status byte                    */
 #define FD_PIPE_ST_DESC   0x01      /* descriptor inside the arena            */
 #define FD_PIPE_ST_BADS   0x02      /* S >= l                                 */
@@ -982,6 +1031,9 @@ extern "C" __global__ void __launch_bounds__( 3 * FD_VERIFY_BLOCK, 1 )
 fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   __shared__ uint4    s_buf[ 2 ][ 4 ][ 10*64 ];       /* phase C / B: a table entry per wave      */
   __shared__ uint32_t s_y[ 2 ][ 4 ][ 24*64 ];         /* phase C / B: u, v, w digit scalars       */
+  __shared__ uint32_t s_lo[ 4*FD_LEN_NB + FD_VERIFY_BLOCK + 2 ];   /* phase A: length order (pipe_len_order) */
+  if( threadIdx.x < 2 ) s_lo[ 4*FD_LEN_NB + FD_VERIFY_BLOCK + threadIdx.x ] = 0u;
+  __syncthreads();
   int role = __builtin_amdgcn_readfirstlane( (int)threadIdx.x >> 8 );   /* 0: phase C, 1: phase B, 2: phase A */
   int tid  = (int)threadIdx.x & (FD_VERIFY_BLOCK - 1);
   int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane( tid >> 6 );
@@ -1014,10 +1066,14 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   if( role == 2 ) {
     /* ---- phase A, batch j ---- */
     uint64_t nn = args.n;
+    uint64_t b0 = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK, di = gid;   /* di: the descriptor this lane verifies */
+    if( a.lsort && b0 + FD_VERIFY_BLOCK <= nn )                       /* full workgroups only: all four waves here */
+      di = b0 + pipe_len_order( len_bucket( args.desc[ gid ] ), wv, lane, s_lo, s_lo + 4*FD_LEN_NB,
+                                s_lo + 4*FD_LEN_NB + FD_VERIFY_BLOCK );
     if( (gid & ~(uint64_t)63) >= nn ) return;
     bool valid = gid < nn;
     fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
-    if( valid ) d = args.desc[ gid ];
+    if( valid ) d = args.desc[ di ];
     uint64_t asz = args.arena_sz;
     bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
                    (uint64_t)d.msg_off + d.msg_sz <= asz;
@@ -1060,6 +1116,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YW + j)*cap ] = y[j];
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_A + j)*cap ] = pub[j];
+      h[ (uint64_t)FD_PH_IDX*cap ] = (uint32_t)di;
     }
     if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)nw;
     FE_FENCE();
@@ -1156,7 +1213,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
     }
   }
-  if( !phb && valid ) a.out_c[ gid ] = (int8_t)code;
+  if( !phb && valid ) a.out_c[ hand[ (uint64_t)FD_PH_IDX*cap + gid ] ] = (int8_t)code;
 #ifdef FD_PHASE_STAMPS
   if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[phb ? 1 : 0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[phb ? 6 : 7], 1ull ); }
 #endif
@@ -1315,11 +1372,6 @@ fd_ed25519_kcache_part_kernel( kpart_args a ) {
 }
 
 /* ------------------------------------------------------------------ length buckets */
-
-__device__ __forceinline__ uint32_t len_bucket( fd_ed25519_desc_t const & d ) {
-  uint32_t b = (64u + (uint32_t)d.msg_sz + 17u + 127u) >> 7;
-  return min( b, (uint32_t)FD_LEN_NB - 1u );
-}
 
 /* Descriptor order by SHA-512 block count inside segments of FD_LEN_SEG
    consecutive descriptors (one 1024-thread workgroup per segment, counting

@@ -1,10 +1,11 @@
 """Same-process A/B of pipelined-launch tuning knobs (dev tool): one context
-per "kb:prio" setting (FD_ED25519_GPU_PIPE_KB = chain windows in phase B,
-FD_ED25519_GPU_PIPE_PRIO = "cba" wave priorities; both read when a context
-first uses the pipe), launches alternated in rounds on the bench's 64K
-config-2 batch; prints the median ms per launch of each.
+per "kb:prio[:lsort]" setting (FD_ED25519_GPU_PIPE_KB = chain windows in phase B,
+FD_ED25519_GPU_PIPE_PRIO = "cba" wave priorities, FD_ED25519_GPU_PIPE_LSORT =
+phase A's length order; read when a context first uses the pipe), launches
+alternated in rounds on the bench's 64K config-2 batch (AB_MSG=var: config 3's
+Uniform{0..1232}-B messages); prints the median ms per launch of each.
 
-  python3 tools/pipe_knob_ab.py 15:000 17:000 13:000 ...
+  python3 tools/pipe_knob_ab.py 15:000 17:000 13:000:0 ...
 """
 import os
 import statistics
@@ -20,7 +21,8 @@ import firedancer_amd as fa  # noqa: E402
 
 knobs = sys.argv[1:] or ["15:000"]
 n = 65536
-arena, desc, sz, expect, _ = bench.build_workload(n, 200, seed=0, n_keys=None)
+msg = None if os.environ.get("AB_MSG") == "var" else 200
+arena, desc, sz, expect, _ = bench.build_workload(n, msg, seed=0, n_keys=None)
 d_arena = torch.from_numpy(arena).cuda()
 d_desc = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
 out = torch.zeros(n, dtype=torch.int8, device="cuda")
@@ -28,9 +30,10 @@ st = torch.cuda.Stream()
 torch.cuda.set_stream(st)
 ctxs = []
 for k in knobs:
-    kb, pr = k.split(":")
+    kb, pr = k.split(":")[:2]
     os.environ["FD_ED25519_GPU_PIPE_KB"] = kb
     os.environ["FD_ED25519_GPU_PIPE_PRIO"] = pr
+    os.environ["FD_ED25519_GPU_PIPE_LSORT"] = k.split(":")[2] if k.count(":") > 1 else "1"
     g = fa.Ed25519Gpu(device_mask=1, max_batch=n)
     g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, out.data_ptr(), stream=st.cuda_stream)
     ctxs.append(g)
