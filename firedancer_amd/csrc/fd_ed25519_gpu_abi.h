@@ -171,6 +171,12 @@ struct fparse_args {
 #define FD_KERN_FEMIT    "fd_frag_emit_kernel"
 #define FD_KERN_FFOLD    "fd_frag_fold_kernel"
 #define FD_KERN_PIPE     "fd_ed25519_verify_pipe_kernel"
+/* Waves per workgroup of the single-lane kernel: one, so the dispatcher
+   refills each SIMD's wave slot as soon as that wave ends (four-wave
+   workgroups held a slot until the workgroup's longest wave ended). */
+#ifndef FD_SL_WAVES
+#define FD_SL_WAVES 1
+#endif
 #define FD_KERN_LSORT    "fd_len_sort_kernel"
 
 /* SHA-block bucketing of one-shot launches above one wave per SIMD

@@ -708,10 +708,10 @@ __device__ __forceinline__ void comb_lds( ge_p3 & acc, uint4 * buf, uint32_t con
    (Q = [v]([S]B - [k]A - R), fd_lattice_dev.h).  The reported code follows
    the reference's check order (fd_ed25519_user.c:157-228): S, decode A,
    decode R, small-order A, small-order R, equation. */
-extern "C" __global__ void __launch_bounds__( FD_VERIFY_BLOCK, FD_VERIFY_WAVES_PER_EU )
+extern "C" __global__ void __launch_bounds__( 64 * FD_SL_WAVES, FD_VERIFY_WAVES_PER_EU )
 fd_ed25519_verify_kernel( verify_args args ) {
-  __shared__ uint4    s_buf[ 4 ][ 10*64 ];     /* a table / comb entry per wave (LDS-DMA) */
-  __shared__ uint32_t s_y[ 4 ][ 24*64 ];       /* per wave: biased u, v, w (8 words each) */
+  __shared__ uint4    s_buf[ FD_SL_WAVES ][ 10*64 ];     /* a table / comb entry per wave (LDS-DMA) */
+  __shared__ uint32_t s_y[ FD_SL_WAVES ][ 24*64 ];       /* per wave: biased u, v, w (8 words each) */
 
   int tid = (int)threadIdx.x;
   int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane( tid >> 6 );
@@ -719,7 +719,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
   uint64_t _st[ FD_NSTAMP ] = { 0, 0, 0, 0, 0, 0, 0, 0 };
 #endif
   STAMP( 0 );
-  uint64_t gid = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + (uint64_t)tid;
+  uint64_t gid = (uint64_t)blockIdx.x * (64u * FD_SL_WAVES) + (uint64_t)tid;
   uint64_t cap = args.vtab_cap;
   /* List form (hot-key cache split): the count is known on the device only;
      whole waves past it leave at once (wave-uniform). */
@@ -1390,9 +1390,9 @@ fd_len_sort_kernel( len_args a ) {
   __syncthreads();
   for( uint32_t j=tid; j<m; j+=1024u ) atomicAdd( &h[ len_bucket( a.desc[ lo + j ] ) ], 1u );
   __syncthreads();
-  if( tid == 0u ) {
+  if( tid == 0u ) {   /* longest first: the segment's last workgroups are its shortest (a shorter launch tail) */
     uint32_t c = 0u;
-    for( int k=0; k<FD_LEN_NB; k++ ) { cur[k] = c; c += h[k]; }
+    for( int k=FD_LEN_NB-1; k>=0; k-- ) { cur[k] = c; c += h[k]; }
   }
   __syncthreads();
   for( uint32_t j=tid; j<m; j+=1024u ) {

@@ -1,11 +1,10 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s3f.log 2>&1 || { tail -40 gpurun_out/gpu_tests_s3f.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_s3f.log
-timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3f.log 2>&1 || { tail -20 gpurun_out/smoke_s3f.log; exit 1; }
-tail -1 gpurun_out/smoke_s3f.log
-timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_s3f.json 2> gpurun_out/bench_driver_s3f.err || { tail -20 gpurun_out/bench_driver_s3f.err; exit 1; }
-cut -c1-200 gpurun_out/bench_driver_s3f.json
-FD_ED25519_GPU_LIB=tools/bin/libfd_ed25519_gpu_stamps.so timeout -k 10 200 python3 tools/timeline.py 65536 30 gpurun_out/timeline_s3f.json > gpurun_out/timeline_s3f.log 2>&1
-bash tools/profile.sh r02s3f
-bash tools/profile_configs.sh r02s3f
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_sl1.log 2>&1 || { tail -40 gpurun_out/gpu_tests_sl1.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_sl1.log
+for r in 1 2; do
+for L in sl4 sl1; do
+echo -n "$L " | tee -a gpurun_out/c3_sl_s3.log
+FD_ED25519_GPU_LIB=tools/bin/lib_$L.so timeout -k 10 300 python3 bench.py --config 3 --steps 10 --warmup 3 --no-cpu 2>/dev/null | tail -1 | cut -c1-140 | tee -a gpurun_out/c3_sl_s3.log
+done
+done

@@ -83,6 +83,12 @@ for b in range(nb):
 rep["simd_last_wave_alone_share"] = float(alone / (nb * 4 * span))
 xcc = (hw >> np.uint64(32)).astype(np.int64)
 rep["cu_end_us_by_xcc"] = {int(x): float(cu_end[xcc[:, 0] == x].mean()) * tick_ns / 1e3 for x in np.unique(xcc[:, 0])}
+clk = cyc / (dur * tick_ns)                                   # per-wave GHz (s_memtime / s_memrealtime)
+rep["by_xcc"] = {int(x): {"clock_ghz": float(np.median(clk[xcc[:, 0] == x])),
+                          "phase_C_dur_us": float((dur[xcc[:, 0] == x][:, 0:4]).mean()) * tick_ns / 1e3,
+                          "phase_C_cycles_k": float((cyc[xcc[:, 0] == x][:, 0:4]).mean()) / 1e3,
+                          "cu_end_us": float(cu_end[xcc[:, 0] == x].mean()) * tick_ns / 1e3}
+                 for x in np.unique(xcc[:, 0])}
 rep["last_wave_role_counts"] = {roles[r]: int(c) for r, c in zip(*np.unique(
     np.argmax(np.stack([end[:, 0:4], end[:, 4:8], end[:, 8:12]], axis=2), axis=2), return_counts=True))}
 print(json.dumps(rep, indent=1))
