@@ -177,6 +177,10 @@ struct fparse_args {
 #ifndef FD_SL_WAVES
 #define FD_SL_WAVES 1
 #endif
+#ifndef FD_SL_WAVES_PER_EU
+#define FD_SL_WAVES_PER_EU 2   /* <= 256 VGPRs (3, i.e. <= 168 VGPRs and 2.5 waves per SIMD by LDS, spilled 27
+                                  dwords and made config 3 8 % slower: profiles/r02/s3/c3_we_s3.log) */
+#endif
 #define FD_KERN_LSORT    "fd_len_sort_kernel"
 
 /* SHA-block bucketing of one-shot launches above one wave per SIMD

@@ -708,7 +708,7 @@ __device__ __forceinline__ void comb_lds( ge_p3 & acc, uint4 * buf, uint32_t con
    (Q = [v]([S]B - [k]A - R), fd_lattice_dev.h).  The reported code follows
    the reference's check order (fd_ed25519_user.c:157-228): S, decode A,
    decode R, small-order A, small-order R, equation. */
-extern "C" __global__ void __launch_bounds__( 64 * FD_SL_WAVES, FD_VERIFY_WAVES_PER_EU )
+extern "C" __global__ void __launch_bounds__( 64 * FD_SL_WAVES, FD_SL_WAVES_PER_EU )
 fd_ed25519_verify_kernel( verify_args args ) {
   __shared__ uint4    s_buf[ FD_SL_WAVES ][ 10*64 ];     /* a table / comb entry per wave (LDS-DMA) */
   __shared__ uint32_t s_y[ FD_SL_WAVES ][ 24*64 ];       /* per wave: biased u, v, w (8 words each) */
