@@ -1,10 +1,10 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_we3.log 2>&1 || { tail -40 gpurun_out/gpu_tests_we3.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_we3.log
-for r in 1 2; do
-for L in we2 we3; do
-echo -n "$L " | tee -a gpurun_out/c3_we_s3.log
-FD_ED25519_GPU_LIB=tools/bin/lib_$L.so timeout -k 10 300 python3 bench.py --config 3 --steps 10 --warmup 3 --no-cpu 2>/dev/null | tail -1 | cut -c1-140 | tee -a gpurun_out/c3_we_s3.log
-done
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s3h.log 2>&1 || { tail -40 gpurun_out/gpu_tests_s3h.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_s3h.log
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3h.log 2>&1 || { tail -20 gpurun_out/smoke_s3h.log; exit 1; }
+tail -1 gpurun_out/smoke_s3h.log
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_s3h.json 2> gpurun_out/bench_driver_s3h.err || { tail -20 gpurun_out/bench_driver_s3h.err; exit 1; }
+cut -c1-200 gpurun_out/bench_driver_s3h.json
+bash tools/profile.sh r02s3h
+bash tools/profile_configs.sh r02s3h
