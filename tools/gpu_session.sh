@@ -1,10 +1,6 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s3h.log 2>&1 || { tail -40 gpurun_out/gpu_tests_s3h.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_s3h.log
-timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3h.log 2>&1 || { tail -20 gpurun_out/smoke_s3h.log; exit 1; }
-tail -1 gpurun_out/smoke_s3h.log
-timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_s3h.json 2> gpurun_out/bench_driver_s3h.err || { tail -20 gpurun_out/bench_driver_s3h.err; exit 1; }
-cut -c1-200 gpurun_out/bench_driver_s3h.json
-bash tools/profile.sh r02s3h
-bash tools/profile_configs.sh r02s3h
+timeout -k 10 300 python -u -m pytest tests/test_pipe.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pipe_order_tests.log 2>&1 || { tail -30 gpurun_out/pipe_order_tests.log; exit 1; }
+tail -1 gpurun_out/pipe_order_tests.log
+timeout -k 10 300 python3 tools/pipe_knob_ab.py 8:000:1:012 8:000:1:102 8:000:1:021 8:000:1:120 8:000:1:201 8:000:1:210 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/order_sweep_s3.log
+timeout -k 10 300 python3 tools/pipe_knob_ab.py 8:000:1:210 8:000:1:201 8:000:1:120 8:000:1:021 8:000:1:102 8:000:1:012 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/order_sweep_s3.log
