@@ -110,3 +110,31 @@ def test_config3_full_size_chunked(oracle):
         s = arena[d["sig_off"]:d["sig_off"] + 64].tobytes()
         p = arena[d["pub_off"]:d["pub_off"] + 32].tobytes()
         assert out[i] == oracle.fdo_verify(m, len(m), s, p, 0)
+
+
+def test_pipe_variable_lengths_length_order(gpu, oracle):
+    """The pipelined form on config-3-like traffic: three 64K batches of
+    Uniform{0..1232}-B messages (a quarter each valid / message-flipped / S >= l
+    / S-flipped), so phase A's in-workgroup length order permutes every full
+    workgroup; every code is the oracle's."""
+    import torch
+    arena, udesc, sz = _config3_records(n_base=2048, seed=37)
+    u = len(udesc)
+    exp_u = np.zeros(u, np.int8)
+    oracle.fdo_verify_descs(arena.ctypes.data_as(ctypes.c_void_p), udesc.ctypes.data_as(ctypes.c_void_p), u,
+                            exp_u.ctypes.data_as(ctypes.c_void_p), 0)
+    n = 65536
+    rng = np.random.default_rng(11)
+    picks = [rng.integers(0, u, size=n) for _ in range(3)]
+    d_arena = torch.from_numpy(arena.copy()).cuda()
+    d_descs = [torch.from_numpy(udesc[p].copy().view(np.uint8)).cuda() for p in picks]
+    outs = [torch.full((n,), 99, dtype=torch.int8, device="cuda:0") for _ in picks]
+    st = torch.cuda.Stream()
+    for d, o in zip(d_descs, outs):
+        gpu.pipe_dev(d_arena.data_ptr(), sz, d.data_ptr(), n, o.data_ptr(), stream=st.cuda_stream)
+    gpu.pipe_flush_dev(stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    for p, o in zip(picks, outs):
+        got = o.cpu().numpy()
+        bad = np.nonzero(got != exp_u[p])[0]
+        assert len(bad) == 0, [(int(i), int(got[i]), int(exp_u[p[i]])) for i in bad[:10]]
