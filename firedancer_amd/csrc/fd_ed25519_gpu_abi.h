@@ -101,7 +101,6 @@ struct pipe_args {
   uint64_t                  kb;         /* windows of the chain in phase B (>= 1) */
   uint64_t                  prio;       /* wave priority of phase C / B / A: bits 0-1 / 2-3 / 4-5 */
   uint64_t                  lsort;      /* phase A: length order inside full workgroups */
-  uint64_t                  order;      /* role of thread third t: bits 2t..2t+1 (0 C, 1 B, 2 A) */
   uint64_t                  set_a, set_b, set_c;
   uint32_t *                hand_a;     /* phase A writes */
   uint8_t *                 st_a;

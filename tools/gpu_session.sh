@@ -1,7 +1,7 @@
 set -e
-mkdir -p gpurun_out/pmc_c3b
-timeout -k 10 400 python -u -m pytest tests/test_gpu_scenarios.py -x -v --timeout 300 --timeout-method thread > gpurun_out/scen_s3.log 2>&1 || { tail -30 gpurun_out/scen_s3.log; exit 1; }
-grep -E "PASS|FAIL" gpurun_out/scen_s3.log | tail -8
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d gpurun_out/pmc_c3b/sq -o pmc -- python3 bench.py --config 3 --steps 3 --warmup 1 --no-cpu > /dev/null 2> gpurun_out/pmc_c3b/sq.err
-echo ok
+mkdir -p gpurun_out
+for r in 1 2; do
+AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_noorder.so tools/bin/lib_cur.so 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_order_s3.log
+AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_cur.so tools/bin/lib_noorder.so 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_order_s3.log
+done
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu 2>/dev/null | cut -c1-160 | tee -a gpurun_out/ab_order_s3.log

@@ -1,8 +1,7 @@
 """Same-process A/B of pipelined-launch tuning knobs (dev tool): one context
-per "kb:prio[:lsort[:order]]" setting (FD_ED25519_GPU_PIPE_KB = chain windows in phase B,
+per "kb:prio[:lsort]" setting (FD_ED25519_GPU_PIPE_KB = chain windows in phase B,
 FD_ED25519_GPU_PIPE_PRIO = "cba" wave priorities, FD_ED25519_GPU_PIPE_LSORT =
-phase A's length order, FD_ED25519_GPU_PIPE_ORDER = roles of the thread
-thirds, oldest first; read when a context first uses the pipe), launches
+phase A's length order; read when a context first uses the pipe), launches
 alternated in rounds on the bench's 64K config-2 batch (AB_MSG=var: config 3's
 Uniform{0..1232}-B messages); prints the median ms per launch of each.
 
@@ -35,7 +34,6 @@ for k in knobs:
     os.environ["FD_ED25519_GPU_PIPE_KB"] = kb
     os.environ["FD_ED25519_GPU_PIPE_PRIO"] = pr
     os.environ["FD_ED25519_GPU_PIPE_LSORT"] = k.split(":")[2] if k.count(":") > 1 else "1"
-    os.environ["FD_ED25519_GPU_PIPE_ORDER"] = k.split(":")[3] if k.count(":") > 2 else "012"
     g = fa.Ed25519Gpu(device_mask=1, max_batch=n)
     g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, out.data_ptr(), stream=st.cuda_stream)
     ctxs.append(g)
