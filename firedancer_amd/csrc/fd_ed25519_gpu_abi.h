@@ -191,7 +191,7 @@ struct fparse_args {
    of the same block count (a wave runs the SHA-512 loop for its longest
    message). */
 #define FD_LEN_NB         16
-#define FD_LEN_SEG        8192
+#define FD_LEN_SEG        16384
 struct len_args {
   fd_ed25519_desc_t const * desc;
   uint64_t                  n;

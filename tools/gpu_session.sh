@@ -1,7 +1,9 @@
 set -e
 mkdir -p gpurun_out
-for r in 1 2; do
-AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_noorder.so tools/bin/lib_cur.so 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_order_s3.log
-AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_cur.so tools/bin/lib_noorder.so 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_order_s3.log
-done
-timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu 2>/dev/null | cut -c1-160 | tee -a gpurun_out/ab_order_s3.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_s3j.log 2>&1 || { tail -40 gpurun_out/gpu_tests_s3j.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_s3j.log
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3j.log 2>&1 || { tail -20 gpurun_out/smoke_s3j.log; exit 1; }
+tail -1 gpurun_out/smoke_s3j.log
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_s3j.json 2> gpurun_out/bench_driver_s3j.err || { tail -20 gpurun_out/bench_driver_s3j.err; exit 1; }
+cut -c1-200 gpurun_out/bench_driver_s3j.json
+bash tools/profile_configs.sh r02s3j
