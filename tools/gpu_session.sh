@@ -1,5 +1,6 @@
 set -e
 mkdir -p gpurun_out
-bash tools/profile.sh r02s3k
-FD_ED25519_GPU_LIB=tools/bin/libfd_ed25519_gpu_stamps.so timeout -k 10 200 python3 tools/timeline.py 65536 30 gpurun_out/timeline_s3k.json > gpurun_out/timeline_s3k.log 2>&1 || true
-echo done
+for r in 1 2; do
+AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_t0.so tools/bin/lib_t1.so 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_ntstore_s3.log
+AB_MODE=pipe timeout -k 10 200 python3 tools/ab_libs.py tools/bin/lib_t1.so tools/bin/lib_t0.so 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_ntstore_s3.log
+done
