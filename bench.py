@@ -28,7 +28,7 @@ Extra keys beside the contract fields:
                   / mean launch time (HIP events on the launch stream),
                   peak = measured v_mad_u64_u32 rate (profiles/r01/valu_probe.json)
                   x 256 CU x 2.4 GHz; traffic = HBM bytes per launch from a
-                  rocprofv3 PMC pass (profiles/r01/pmc_traffic.json, gfx950 FETCH_SIZE x2 correction) or null.
+                  rocprofv3 PMC pass (profiles/<PROFILE_ROUND>/pmc_traffic.json, gfx950 FETCH_SIZE x2 correction) or null.
   cpu_baseline -- the reference fd_ed25519_verify (AVX-512 build when the host
                   has avx512ifma, else the portable build) compiled from the
                   reference sources (oracle/_ref), on a bounded sample of the
@@ -387,7 +387,7 @@ def main():
                 "value_with_drain": n * args.steps / (dt + drain),
             }
         # The same launch against the HBM roofline (not the bound: ~1/6 of the ~8 TB/s peak),
-        # from the PMC-measured bytes per launch of profiles/r01/pmc_traffic.json.
+        # from the PMC-measured bytes per launch of profiles/<PROFILE_ROUND>/pmc_traffic.json.
         t = pmc_traffic(n, kname) if args.config == 2 else None
         if t:
             gbs = t / (launch_ms * 1e-3) / 1e9
