@@ -28,7 +28,12 @@ Extra keys beside the contract fields:
                   / mean launch time (HIP events on the launch stream),
                   peak = measured v_mad_u64_u32 rate (profiles/r01/valu_probe.json)
                   x 256 CU x 2.4 GHz; traffic = HBM bytes per launch from a
-                  rocprofv3 PMC pass (profiles/<PROFILE_ROUND>/pmc_traffic.json, gfx950 FETCH_SIZE x2 correction) or null.
+                  rocprofv3 PMC pass of this very build (the newest profiles/rNN/
+                  pmc_traffic.json whose code-object hash matches the loaded library's
+                  fd_ed25519_gpu_build_id; gfx950 FETCH_SIZE x2 correction) or null.
+  warmup_detail -- the untimed steps before the timed ones: prime steps (back-to-back
+                  launches for --prime-ms, so the clock has left its idle ramp) and
+                  the --warmup steps; build -- the library's build id.
   cpu_baseline -- the reference fd_ed25519_verify (AVX-512 build when the host
                   has avx512ifma, else the portable build) compiled from the
                   reference sources (oracle/_ref), on a bounded sample of the
@@ -110,20 +115,31 @@ def valu_peak():
     return rate * 64 * N_CU * NOMINAL_GHZ * 1e9
 
 
-PROFILE_ROUND = "r02"
+def profile_rounds():
+    """profiles/rNN directories, newest round first."""
+    base = os.path.join(REPO, "profiles")
+    rs = [d for d in os.listdir(base) if d.startswith("r") and d[1:].isdigit()] if os.path.isdir(base) else []
+    return sorted(rs, key=lambda d: int(d[1:]), reverse=True)
 
 
-def pmc_traffic(n, kernel):
-    """HBM bytes per launch of this kernel at this batch size, from the
-    committed PMC summary of this round (tools/profile.sh ->
-    tools/summarize_profile.py), or None."""
-    path = os.path.join(REPO, "profiles", PROFILE_ROUND, "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    d = json.load(open(path))
-    if d.get("batch") != n or d.get("kernel") != kernel:
-        return None
-    return d.get("hbm_bytes_per_launch")
+def pmc_traffic(n, kernel, code):
+    """HBM bytes per launch of this kernel at this batch size from the newest
+    committed PMC summary (tools/profile.sh -> tools/summarize_profile.py,
+    profiles/rNN/pmc_traffic.json) that was measured on THIS build: its
+    "build" entry's code hash must equal the loaded library's
+    (fd_ed25519_gpu_build_id).  Returns (bytes or None, the file used or why
+    none was)."""
+    for r in profile_rounds():
+        path = os.path.join(REPO, "profiles", r, "pmc_traffic.json")
+        if not os.path.exists(path):
+            continue
+        d = json.load(open(path))
+        if d.get("batch") != n or d.get("kernel") != kernel:
+            continue
+        if (d.get("build") or {}).get("code") != code:
+            continue
+        return d.get("hbm_bytes_per_launch"), "profiles/%s/pmc_traffic.json" % r
+    return None, "no committed PMC profile of code object %s (%s, batch %d)" % (code, kernel, n)
 
 
 def cpu_baseline(arena, desc, expect, budget_s=10.0):
@@ -353,6 +369,8 @@ def main():
     if rank == 0:
         peak = valu_peak()
         achieved = W_MAC * n / (launch_ms * 1e-3)
+        build = fa.build_id()
+        traffic, traffic_src = pmc_traffic(n, kname, build.get("code")) if args.config == 2 else (None, "config 2 only")
         line = {
             "metric": "Ed25519 verifies/sec",
             "value": value,
@@ -370,10 +388,14 @@ def main():
                        "msg_sz": args.msg_sz if args.config == 2 else None, "parallelism": "shard-per-gpu x%d" % world},
             "roofline": {"bound": "valu-int32", "achieved": achieved / 1e12, "peak": peak / 1e12,
                          "unit": "T MAC/s (32x32->64 multiply-adds, W=%.4g per verify)" % W_MAC,
-                         "frac": achieved / peak, "traffic": pmc_traffic(n, kname) if args.config == 2 else None,
+                         "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel_ms": launch_ms},
             "cpu_baseline": None,
-            "prime_steps": prime,
+            "warmup_detail": {"prime_steps": prime, "prime_ms": args.prime_ms, "warmup_steps": args.warmup,
+                              "untimed_steps_total": prime + args.warmup,
+                              "note": "prime steps run back to back for prime_ms first (the clock ramps from idle), "
+                                      "then the warmup steps; none of them is timed"},
+            "build": build,
         }
         if pipe:
             line["pipeline"] = {
@@ -386,9 +408,9 @@ def main():
                 "drain_ms": drain * 1e3,
                 "value_with_drain": n * args.steps / (dt + drain),
             }
-        # The same launch against the HBM roofline (not the bound: ~1/6 of the ~8 TB/s peak),
-        # from the PMC-measured bytes per launch of profiles/<PROFILE_ROUND>/pmc_traffic.json.
-        t = pmc_traffic(n, kname) if args.config == 2 else None
+        # The same launch against the HBM roofline (not the bound: ~1/4 of the ~8 TB/s peak),
+        # from the PMC-measured bytes per launch of this build's committed profile.
+        t = traffic
         if t:
             gbs = t / (launch_ms * 1e-3) / 1e9
             line["roofline_hbm"] = {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",

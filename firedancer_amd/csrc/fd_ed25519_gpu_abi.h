@@ -118,6 +118,7 @@ struct pipe_args {
   int8_t const *            code_c;
   uint64_t                  n_c;        /* 0: no batch in phase C */
   int8_t *                  out_c;      /* the codes of batch j-2 */
+  uint32_t *                err;        /* host-mapped error word: set to 1 when a phase-A wait expires */
 };
 
 struct kpart_args {
@@ -156,6 +157,27 @@ struct fparse_args {
   int8_t const *                 code;       /* fold: per-descriptor codes */
 };
 
+/* Shred Merkle roots on the GPU (fd_shred_root_kernel, fd_shred_verify.cpp):
+   one job per shred whose signature is checked -- the leaf is SHA-256 of
+   "\0SOLANA_MERKLE_SHREDS_LEAF" || arena[leaf_off, leaf_off + leaf_len), the
+   proof's `depth` 20-byte siblings at arena + proof_off climb it by the bits
+   of idx, and the 32-byte root goes to arena[out_off, out_off + 32). */
+typedef struct {
+  uint32_t leaf_off;
+  uint32_t leaf_len;
+  uint32_t proof_off;
+  uint32_t out_off;
+  uint16_t depth;
+  uint16_t idx;
+} fd_shred_job_t;
+
+struct shred_root_args {
+  uint8_t *                 arena;     /* device copy; roots written into it */
+  uint64_t                  arena_sz;
+  fd_shred_job_t const *    job;
+  uint64_t                  n;
+};
+
 /* Kernel symbols in the code object (extern "C"). */
 #define FD_KERN_VERIFY   "fd_ed25519_verify_kernel"
 #define FD_KERN_VPAIR    "fd_ed25519_verify_pair_kernel"
@@ -171,6 +193,8 @@ struct fparse_args {
 #define FD_KERN_FEMIT    "fd_frag_emit_kernel"
 #define FD_KERN_FFOLD    "fd_frag_fold_kernel"
 #define FD_KERN_PIPE     "fd_ed25519_verify_pipe_kernel"
+#define FD_KERN_SHA256   "fd_sha256_batch_kernel"
+#define FD_KERN_SROOT    "fd_shred_root_kernel"
 /* Waves per workgroup of the single-lane kernel: one, so the dispatcher
    refills each SIMD's wave slot as soon as that wave ends (four-wave
    workgroups held a slot until the workgroup's longest wave ended). */

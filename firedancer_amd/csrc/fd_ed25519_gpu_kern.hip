@@ -21,6 +21,7 @@
 #include "fd_f25519_dev.h"
 #include "fd_curve25519_dev.h"
 #include "fd_sha512_dev.h"
+#include "fd_sha256_dev.h"
 #include "fd_scalar_dev.h"
 #include "fd_lattice_dev.h"
 
@@ -981,8 +982,13 @@ __device__ __forceinline__ uint32_t len_bucket( fd_ed25519_desc_t const & d ) {
    takes.  The four waves wait for each other on LDS counters zeroed by the
    workgroup's barrier at kernel start (bounded waits: all four are resident
    in the workgroup, so they arrive). */
+#ifdef FD_DIAG_LSORT_TIMEOUT
+#define FD_LSORT_SPIN 0u            /* diagnostic build: every wait that is not already met expires */
+#else
+#define FD_LSORT_SPIN (1u << 20)
+#endif
 __device__ __forceinline__ uint32_t pipe_len_order( uint32_t key, int w, int lane, uint32_t * wh, uint32_t * perm,
-                                                    uint32_t * flag ) {
+                                                    uint32_t * flag, uint32_t * err ) {
   uint64_t below = (1ull << lane) - 1ull;
   uint32_t mine = 0, rank = 0;
 #pragma unroll 1
@@ -994,8 +1000,14 @@ __device__ __forceinline__ uint32_t pipe_len_order( uint32_t key, int w, int lan
   if( lane < FD_LEN_NB ) wh[ w*FD_LEN_NB + lane ] = mine;
   __builtin_amdgcn_fence( __ATOMIC_RELEASE, "workgroup" );
   if( lane == 0 ) __hip_atomic_fetch_add( &flag[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP );
-  for( uint32_t i=0; i<(1u<<20) && __hip_atomic_load( &flag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u; i++ )
+  uint32_t i;
+  for( i=0; i<FD_LSORT_SPIN && __hip_atomic_load( &flag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u; i++ )
     __builtin_amdgcn_s_sleep( 1 );
+  /* an expired wait (impossible while the four waves are co-resident, as
+     one workgroup's waves are) leaves the counts partial: the order below is
+     then not a permutation, so the launch reports it (the host turns the
+     error word into FD_ED25519_GPU_ERR_LAUNCH) instead of returning codes */
+  int late = __hip_atomic_load( &flag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u;
   __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "workgroup" );
   uint32_t pos = rank;
 #pragma unroll 1
@@ -1005,13 +1017,15 @@ __device__ __forceinline__ uint32_t pipe_len_order( uint32_t key, int w, int lan
     uint32_t pre = (w > 0 ? c0 : 0u) + (w > 1 ? c1 : 0u) + (w > 2 ? c2 : 0u);
     pos += b < key ? tot : (b == key ? pre : 0u);
   }
-  perm[ pos ] = (uint32_t)(w*64 + lane);
+  perm[ pos & (FD_VERIFY_BLOCK - 1u) ] = (uint32_t)(w*64 + lane);
   __builtin_amdgcn_fence( __ATOMIC_RELEASE, "workgroup" );
   if( lane == 0 ) __hip_atomic_fetch_add( &flag[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP );
-  for( uint32_t i=0; i<(1u<<20) && __hip_atomic_load( &flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u; i++ )
+  for( i=0; i<FD_LSORT_SPIN && __hip_atomic_load( &flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u; i++ )
     __builtin_amdgcn_s_sleep( 1 );
+  late |= __hip_atomic_load( &flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u;
   __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "workgroup" );
-  return perm[ w*64 + lane ];
+  if( late && lane == 0 && err ) __hip_atomic_store( err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+  return perm[ w*64 + lane ] & (FD_VERIFY_BLOCK - 1u);   /* in the workgroup's range whatever happened */
 }
 
 #define FD_PIPE_ST_VALID  0x80      /* phase A status byte                    */
@@ -1068,12 +1082,16 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 
   if( role == 2 ) {
     /* ---- phase A, batch j ---- */
-    uint64_t nn = args.n;
+    uint64_t nn = args.n;                                               /* args.cnt: a device-side count <= n */
+    if( args.cnt ) nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)*args.cnt ) );
     uint64_t b0 = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK, di = gid;   /* di: the descriptor this lane verifies */
     if( a.lsort && b0 + FD_VERIFY_BLOCK <= nn )                       /* full workgroups only: all four waves here */
       di = b0 + pipe_len_order( len_bucket( args.desc[ gid ] ), wv, lane, s_lo, s_lo + 4*FD_LEN_NB,
-                                s_lo + 4*FD_LEN_NB + FD_VERIFY_BLOCK );
-    if( (gid & ~(uint64_t)63) >= nn ) return;
+                                s_lo + 4*FD_LEN_NB + FD_VERIFY_BLOCK, a.err );
+    if( (gid & ~(uint64_t)63) >= nn ) {
+      if( gid < args.n ) a.st_a[ gid ] = 0u;             /* past a device-side count: no batch slot */
+      return;
+    }
     bool valid = gid < nn;
     fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
     if( valid ) d = args.desc[ di ];
@@ -1123,8 +1141,8 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
     }
     if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)nw;
     FE_FENCE();
-    if( valid )
-      a.st_a[ gid ] = (uint8_t)(FD_PIPE_ST_VALID | (desc_ok ? FD_PIPE_ST_DESC : 0) | (bad_s ? FD_PIPE_ST_BADS : 0) |
+    if( gid < args.n )
+      a.st_a[ gid ] = !valid ? (uint8_t)0 : (uint8_t)(FD_PIPE_ST_VALID | (desc_ok ? FD_PIPE_ST_DESC : 0) | (bad_s ? FD_PIPE_ST_BADS : 0) |
                                 (un ? FD_PIPE_ST_UNEG : 0));
 #ifdef FD_PHASE_STAMPS
     if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[5], 1ull ); }
@@ -1141,10 +1159,11 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   bool phb = role == 1;
   uint64_t nx = phb ? a.n_b : a.n_c;
   if( (gid & ~(uint64_t)63) >= nx ) return;
-  bool valid = gid < nx;
   uint64_t set = phb ? a.set_b : a.set_c;
   uint32_t const * hand = phb ? a.hand_b : a.hand_c;
-  int ps = valid ? (int)(phb ? a.st_b : a.st_c)[ gid ] : 0;
+  int ps = gid < nx ? (int)(phb ? a.st_b : a.st_c)[ gid ] : 0;
+  bool valid = (ps & FD_PIPE_ST_VALID) != 0;            /* phase A marked the batch's slots */
+  if( !__ballot( valid ) ) return;                      /* a wave past a device-side count */
   int code;
   if( phb ) {
     bool desc_ok = (ps & FD_PIPE_ST_DESC) != 0, bad_s = (ps & FD_PIPE_ST_BADS) != 0;
@@ -1281,6 +1300,83 @@ fd_sha512_batch_kernel( uint8_t const * arena, uint64_t arena_sz, fd_sha512_gpu_
   for( int q=0; q<4; q++ )
     o[q] = make_uint4( sha_bswap32( (uint32_t)(h[2*q]   >> 32) ), sha_bswap32( (uint32_t)h[2*q]   ),
                        sha_bswap32( (uint32_t)(h[2*q+1] >> 32) ), sha_bswap32( (uint32_t)h[2*q+1] ) );
+}
+
+/* ------------------------------------------------------------------ SHA-256 batch */
+
+/* Batched SHA-256, one message per lane (replaces fd_sha256_hash,
+   src/ballet/sha256/fd_sha256.c, and the fd_sha256_batch_* API of
+   src/ballet/sha256/fd_sha256.h): digest i = SHA-256( arena[off, off + sz) )
+   to out[32 i .. 32 i + 31]. */
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_sha256_batch_kernel( uint8_t const * arena, uint64_t arena_sz, fd_sha512_gpu_msg_t const * msg, uint64_t n,
+                        uint8_t * out ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  fd_sha512_gpu_msg_t m = msg[ i ];
+  uint32_t lim_dw = (uint32_t)((arena_sz + 3u) >> 2) + 1u;
+  uint32_t const pw[ 8 ] = { 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u };
+  uint32_t h[ 8 ];
+  sha256_span( h, pw, 0u, arena, m.off, m.sz, lim_dw );
+  uint4 * o = (uint4 *)(out + 32u*i);
+  o[0] = make_uint4( s256_bswap( h[0] ), s256_bswap( h[1] ), s256_bswap( h[2] ), s256_bswap( h[3] ) );
+  o[1] = make_uint4( s256_bswap( h[4] ), s256_bswap( h[5] ), s256_bswap( h[6] ), s256_bswap( h[7] ) );
+}
+
+/* The shred Merkle roots of the FEC resolver's signature check
+   (src/disco/shred/fd_fec_resolver.c:334-399; fd_bmtree_hash_leaf /
+   fd_bmtree_commitp_insert_with_proof, src/ballet/bmtree/fd_bmtree.c:
+   385-420), one shred per lane: the leaf over the protected bytes (~18
+   blocks), then per proof layer one node hash of 26 + 20 + 20 bytes (two
+   blocks), left / right by the index bit; the 32-byte root is written into
+   the device arena where the verify kernel reads it as the message. */
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_shred_root_kernel( shred_root_args a ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= a.n ) return;
+  fd_shred_job_t j = a.job[ i ];
+  uint32_t lim_dw = (uint32_t)((a.arena_sz + 3u) >> 2) + 1u;
+  uint32_t const leaf[ 8 ] = { 0x00534f4cu, 0x414e415fu, 0x4d45524bu, 0x4c455f53u,      /* "\0SOLANA_MERKLE_SHREDS_LEAF" */
+                               0x48524544u, 0x535f4c45u, 0x41460000u, 0x00000000u };
+  uint32_t h[ 8 ];
+  sha256_span( h, leaf, 26u, a.arena, j.leaf_off, j.leaf_len, lim_dw );
+  uint32_t const np[ 7 ] = { 0x01534f4cu, 0x414e415fu, 0x4d45524bu, 0x4c455f53u,      /* "\1SOLANA_MERKLE_SHREDS_NODE" */
+                             0x48524544u, 0x535f4e4fu, 0x44450000u };
+#pragma unroll 1
+  for( uint32_t l=0; l<j.depth; l++ ) {
+    uint32_t sib[ 5 ];
+    load_words<5>( sib, a.arena, j.proof_off + 20u*l, lim_dw );
+    uint32_t nd[ 5 ], L[ 5 ], R[ 5 ];
+    int right = (j.idx >> l) & 1u;                 /* this node is the right child */
+#pragma unroll
+    for( int k=0; k<5; k++ ) {
+      nd[k] = h[k];                                /* a node is the hash's first 20 bytes */
+      uint32_t sk = s256_bswap( sib[k] );
+      L[k] = right ? sk : nd[k];
+      R[k] = right ? nd[k] : sk;
+    }
+    uint32_t W[ 16 ];
+#pragma unroll
+    for( int k=0; k<6; k++ ) W[k] = np[k];
+    W[6]  = np[6] | (L[0] >> 16);
+#pragma unroll
+    for( int k=0; k<4; k++ ) W[7+k] = (L[k] << 16) | (L[k+1] >> 16);
+    W[11] = (L[4] << 16) | (R[0] >> 16);
+#pragma unroll
+    for( int k=0; k<4; k++ ) W[12+k] = (R[k] << 16) | (R[k+1] >> 16);
+    sha256_init_state( h );
+    sha256_compress( h, W );
+    W[0] = (R[4] << 16) | 0x8000u;
+#pragma unroll
+    for( int k=1; k<15; k++ ) W[k] = 0u;
+    W[15] = 66u * 8u;
+    sha256_compress( h, W );
+  }
+  uint8_t * o = a.arena + j.out_off;
+#pragma unroll
+  for( int k=0; k<8; k++ ) {
+    o[4*k] = (uint8_t)(h[k] >> 24); o[4*k+1] = (uint8_t)(h[k] >> 16); o[4*k+2] = (uint8_t)(h[k] >> 8); o[4*k+3] = (uint8_t)h[k];
+  }
 }
 
 /* ------------------------------------------------------------------ hot-key cache */

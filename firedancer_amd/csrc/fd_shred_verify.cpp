@@ -16,16 +16,25 @@
        || left[20] || right[20] ), left / right by the index bits
        (fd_bmtree.c:385-420 on a fresh tree)
      fd_ed25519_verify( root, 32, signature, leader )            (:399)
-   Here the host does all of that but the verify (the SHA-256 work is ~20
-   compression blocks per shred), writes each root into the caller's aux
-   region and emits one descriptor per shred; whether a shred opens a set
-   (the resolver's maps) is the caller's state.  SHA-256: FIPS 180-4, our
-   own code. */
+   fd_ed25519_gpu_shred_walk does all of that but the verify on the host
+   (the SHA-256 work is ~20 compression blocks per shred; FIPS 180-4, our
+   own code), writes each root into the caller's aux region and emits one
+   descriptor per shred.  fd_ed25519_gpu_shred_verify keeps only the checks
+   on the host: the roots are computed on the GPU (fd_shred_root_kernel, one
+   shred per lane) right before the verify kernel reads them, and copied
+   back into aux.  Whether a shred opens a set (the resolver's maps) is the
+   caller's state. */
 
+#include <stdlib.h>
 #include <string.h>
 #include <vector>
 
-#include "../../include/fd_ed25519_gpu.h"
+#include "fd_ed25519_gpu_abi.h"
+
+/* GPU half (fd_ed25519_gpu_host.cpp) */
+extern "C" int fd_ed25519_gpu_merkle_verify( fd_ed25519_gpu_t * ctx, uint8_t * arena, uint64_t arena_sz, uint64_t aux_off,
+                                             uint64_t aux_sz, fd_shred_job_t const * job, fd_ed25519_desc_t const * desc,
+                                             uint64_t n, int8_t * code );
 
 /* ---- SHA-256 ---- */
 
@@ -139,10 +148,12 @@ static inline uint64_t bmtree_depth( uint64_t leaves ) {
   return (uint64_t)(63 - __builtin_clzll( leaves - 1u )) + 2u;
 }
 
-extern "C" int64_t
-fd_ed25519_gpu_shred_walk( uint8_t * arena, uint64_t arena_sz, uint64_t aux_off, uint64_t aux_cap,
-                           fd_ed25519_gpu_span_t const * shred, uint32_t const * key_off, uint64_t n,
-                           fd_ed25519_desc_t * desc, uint64_t desc_cap, int64_t * shred_desc ) {
+/* The walk; job == NULL: the roots are hashed here into aux, else job[k]
+   describes descriptor k's root for the GPU (aux left untouched). */
+static int64_t
+shred_walk( uint8_t * arena, uint64_t arena_sz, uint64_t aux_off, uint64_t aux_cap,
+            fd_ed25519_gpu_span_t const * shred, uint32_t const * key_off, uint64_t n,
+            fd_ed25519_desc_t * desc, uint64_t desc_cap, int64_t * shred_desc, fd_shred_job_t * job ) {
   if( (n && (!shred || !key_off || !shred_desc)) || (!arena && arena_sz) || (desc_cap && !desc) ) return FD_ED25519_GPU_ERR_ARG;
   if( arena_sz > 0xffffffffull || aux_off > arena_sz || aux_cap > arena_sz - aux_off ) return FD_ED25519_GPU_ERR_ARG;
   for( uint64_t j=0; j<n; j++ ) {
@@ -179,19 +190,26 @@ fd_ed25519_gpu_shred_walk( uint8_t * arena, uint64_t arena_sz, uint64_t aux_off,
     if( 32u > aux_cap - (nd * 32u) ) return FD_ED25519_GPU_ERR_ARG;
     if( nd >= desc_cap ) return FD_ED25519_GPU_ERR_ARG;
     /* leaf, then the proof climbed (the shred's proof sits at its fixed size's end) */
-    uint8_t node[ 32 ];
-    sha256_3( node, LEAF_PREFIX, 26, b + 64, protect, NULL, 0 );
     uint64_t fixed = (variant & 0x40) ? SHRED_MAX_SZ : ((variant & 0xf0) == 0x80 ? SHRED_MIN_SZ : rd16( b + 0x56 ));
     uint8_t const * proof = b + fixed - depth * SHRED_NODE_SZ;
-    for( uint64_t l=0; l<depth; l++ ) {
-      uint8_t pair[ 2 * SHRED_NODE_SZ ];
-      uint8_t const * sib = proof + SHRED_NODE_SZ * l;
-      if( !((idx >> l) & 1u) ) { memcpy( pair, node, SHRED_NODE_SZ ); memcpy( pair + SHRED_NODE_SZ, sib, SHRED_NODE_SZ ); }
-      else                     { memcpy( pair, sib, SHRED_NODE_SZ ); memcpy( pair + SHRED_NODE_SZ, node, SHRED_NODE_SZ ); }
-      sha256_3( node, NODE_PREFIX, 26, pair, 2 * SHRED_NODE_SZ, NULL, 0 );
-    }
     uint64_t at = aux_off + nd * 32u;
-    memcpy( arena + at, node, 32 );
+    if( job ) {
+      fd_shred_job_t * jb = &job[ nd ];
+      jb->leaf_off = (uint32_t)(shred[ j ].off + 64u); jb->leaf_len = (uint32_t)protect;
+      jb->proof_off = (uint32_t)(proof - arena); jb->out_off = (uint32_t)at;
+      jb->depth = (uint16_t)depth; jb->idx = (uint16_t)idx;
+    } else {
+      uint8_t node[ 32 ];
+      sha256_3( node, LEAF_PREFIX, 26, b + 64, protect, NULL, 0 );
+      for( uint64_t l=0; l<depth; l++ ) {
+        uint8_t pair[ 2 * SHRED_NODE_SZ ];
+        uint8_t const * sib = proof + SHRED_NODE_SZ * l;
+        if( !((idx >> l) & 1u) ) { memcpy( pair, node, SHRED_NODE_SZ ); memcpy( pair + SHRED_NODE_SZ, sib, SHRED_NODE_SZ ); }
+        else                     { memcpy( pair, sib, SHRED_NODE_SZ ); memcpy( pair + SHRED_NODE_SZ, node, SHRED_NODE_SZ ); }
+        sha256_3( node, NODE_PREFIX, 26, pair, 2 * SHRED_NODE_SZ, NULL, 0 );
+      }
+      memcpy( arena + at, node, 32 );
+    }
     fd_ed25519_desc_t d;
     d.sig_off = shred[ j ].off;
     d.pub_off = key_off[ j ];
@@ -205,6 +223,13 @@ fd_ed25519_gpu_shred_walk( uint8_t * arena, uint64_t arena_sz, uint64_t aux_off,
   return (int64_t)nd;
 }
 
+extern "C" int64_t
+fd_ed25519_gpu_shred_walk( uint8_t * arena, uint64_t arena_sz, uint64_t aux_off, uint64_t aux_cap,
+                           fd_ed25519_gpu_span_t const * shred, uint32_t const * key_off, uint64_t n,
+                           fd_ed25519_desc_t * desc, uint64_t desc_cap, int64_t * shred_desc ) {
+  return shred_walk( arena, arena_sz, aux_off, aux_cap, shred, key_off, n, desc, desc_cap, shred_desc, NULL );
+}
+
 extern "C" int
 fd_ed25519_gpu_shred_verify( fd_ed25519_gpu_t * ctx, uint8_t * arena, uint64_t arena_sz, uint64_t aux_off,
                              uint64_t aux_cap, fd_ed25519_gpu_span_t const * shred, uint32_t const * key_off,
@@ -212,11 +237,18 @@ fd_ed25519_gpu_shred_verify( fd_ed25519_gpu_t * ctx, uint8_t * arena, uint64_t a
   if( !ctx || (n && !out) ) return FD_ED25519_GPU_ERR_ARG;
   std::vector<fd_ed25519_desc_t> desc( n ? n : 1u );
   std::vector<int64_t> sd( n ? n : 1u );
-  int64_t nd = fd_ed25519_gpu_shred_walk( arena, arena_sz, aux_off, aux_cap, shred, key_off, n, desc.data(), n, sd.data() );
+  /* FD_ED25519_GPU_SHRED_HOST_HASH=1: the roots on the host (A/B runs) */
+  char const * e = getenv( "FD_ED25519_GPU_SHRED_HOST_HASH" );
+  int host_hash = e && e[0] == '1';
+  std::vector<fd_shred_job_t> job( host_hash ? 1u : (n ? n : 1u) );
+  int64_t nd = shred_walk( arena, arena_sz, aux_off, aux_cap, shred, key_off, n, desc.data(), n, sd.data(),
+                           host_hash ? NULL : job.data() );
   if( nd < 0 ) return (int)nd;
   std::vector<int8_t> code( nd ? (size_t)nd : 1u );
   if( nd ) {
-    int err = fd_ed25519_verify_batch_gpu( ctx, arena, arena_sz, desc.data(), (uint64_t)nd, code.data() );
+    int err = host_hash ? fd_ed25519_verify_batch_gpu( ctx, arena, arena_sz, desc.data(), (uint64_t)nd, code.data() )
+                        : fd_ed25519_gpu_merkle_verify( ctx, arena, arena_sz, aux_off, 32u * (uint64_t)nd, job.data(),
+                                                        desc.data(), (uint64_t)nd, code.data() );
     if( err ) return err;
   }
   for( uint64_t j=0; j<n; j++ ) out[ j ] = sd[ j ] >= 0 ? (int)code[ (size_t)sd[ j ] ] : (int)sd[ j ];

@@ -5,12 +5,12 @@
 
    Batching policy: a batch is cut at the ring end and at a frag-area wrap
    (so its bytes are one contiguous span for the copy to HBM) and holds at
-   most max_batch frags.  With the GPU idle any available frags go at once;
-   with one batch outstanding the next is submitted when at least
-   max_batch/2 frags wait, or when the outstanding batch has completed --
-   so under load batches grow to max_batch and the host parse of one batch
-   overlaps the GPU work of the previous one (two in flight), and at low
-   load latency stays at one batch. */
+   most max_batch frags.  With nothing outstanding any available frags go at
+   once; with batches outstanding the next is submitted when at least
+   max_batch/2 frags wait -- so under load batches grow to max_batch and up
+   to three are in flight (the pipelined kernel runs one phase of each per
+   launch), and at low load latency stays at one batch: the stage finishes
+   a lone batch with drain launches as soon as the GPU is idle. */
 
 #include "../../include/fd_ed25519_gpu.h"
 #include "../../include/fd_verify_offload.h"
@@ -32,27 +32,28 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
   if( !off || !ctx || !tc || !max_batch ) return FD_ED25519_GPU_ERR_ARG;
   fd_ed25519_gpu_stage_t * st = fd_ed25519_gpu_stage_new( ctx, tc, max_batch, threads );
   if( !st ) return FD_ED25519_GPU_ERR_OOM;
-  uint64_t q_seq[ 2 ], q_cnt[ 2 ];   /* outstanding batches, oldest first */
+  enum { DEPTH = 3 };                /* the stage's batches in flight */
+  uint64_t q_seq[ DEPTH ], q_cnt[ DEPTH ];   /* outstanding batches, oldest first */
   int q = 0;
   uint64_t done = fd_verify_offload_done_seq( off );
   uint64_t s_batches = 0, s_frags = 0, s_max = 0, s_idle = 0, s_sub_ns = 0, s_poll_ns = 0, t_first = 0, t_last = 0;
   int err = FD_ED25519_GPU_OK;
   uint8_t * dc = fd_verify_offload_dcache( off );
   uint64_t dsz = fd_verify_offload_dcache_sz( off );
-  /* Private snapshots of the frag records of the (up to two) batches in
+  /* Private snapshots of the frag records of the (up to three) batches in
      flight: the client can rewrite the shared ring at any time, so the stage
      parses (and bounds-checks against dsz) a copy it alone owns. */
-  std::vector<fd_ed25519_gpu_frag_t> snap[ 2 ];
-  snap[ 0 ].resize( max_batch ); snap[ 1 ].resize( max_batch );
+  std::vector<fd_ed25519_gpu_frag_t> snap[ DEPTH ];
+  for( int k=0; k<DEPTH; k++ ) snap[ k ].resize( max_batch );
   int snap_next = 0;
   for(;;) {
     int progressed = 0;
     uint64_t first, avail = fd_verify_offload_avail( off, &first );
-    if( q < 2 && avail && (q == 0 || avail >= max_batch/2u) ) {
+    if( q < DEPTH && avail && (q == 0 || avail >= max_batch/2u) ) {
       uint64_t m = avail < max_batch ? avail : max_batch;
       fd_ed25519_gpu_frag_t * f = snap[ snap_next ].data();
       memcpy( f, fd_verify_offload_frag_laddr( off, first ), m * sizeof(fd_ed25519_gpu_frag_t) );
-      snap_next ^= 1;
+      snap_next = (snap_next + 1) % DEPTH;
       for( uint64_t j=1; j<m; j++ ) if( f[ j ].off < f[ j-1 ].off ) { m = j; break; }   /* frag-area wrap */
       uint64_t t0 = now_ns();
       if( !t_first ) t_first = t0;
@@ -76,7 +77,8 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
         s_poll_ns += t_last - t0;
         done = q_seq[ 0 ] + q_cnt[ 0 ];
         fd_verify_offload_complete( off, done );
-        q_seq[ 0 ] = q_seq[ 1 ]; q_cnt[ 0 ] = q_cnt[ 1 ]; q--;
+        for( int k=1; k<q; k++ ) { q_seq[ k-1 ] = q_seq[ k ]; q_cnt[ k-1 ] = q_cnt[ k ]; }
+        q--;
         progressed = 1;
       } else if( r != FD_ED25519_GPU_PENDING ) { err = r; break; }
     }

@@ -250,8 +250,14 @@ extern "C" int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t * ctx, uint8_t cons
                                             fd_ed25519_gpu_frag_t const * frag, uint64_t n, int8_t * status,
                                             uint64_t * tag );
 extern "C" int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t * ctx, int block );
+extern "C" int fd_ed25519_gpu_poll_block( fd_ed25519_gpu_t * ctx );
 extern "C" uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx );
 extern "C" int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n );
+
+/* Batches outstanding at once: three, the depth of the pipelined verify
+   kernel (fd_ed25519_gpu_submit / fd_ed25519_gpu_frags_submit take up to
+   three and finish each one two launches after its own). */
+#define FD_VS_DEPTH 3
 
 struct vs_batch {
   int                            state = 0; /* 0 free, 1 parsed, 2 on the GPU, 3 GPU done / nothing to verify */
@@ -279,8 +285,8 @@ struct fd_ed25519_gpu_stage {
   int                       threads;
   int                       devparse;      /* parse frags on the GPU when the context has room */
   int                       head;          /* oldest pending slot */
-  int                       pending;       /* 0..2 */
-  vs_batch                  b[ 2 ];
+  int                       pending;       /* 0..FD_VS_DEPTH */
+  vs_batch                  b[ FD_VS_DEPTH ];
 };
 
 /* Parse frags [lo, hi) of a batch into per-frag status / tag / count / fields. */
@@ -486,12 +492,12 @@ fd_ed25519_gpu_stage_warm( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, u
   static uint8_t const zero[ 64 ] = { 0 };
   if( !arena_sz ) { arena = zero; arena_sz = sizeof(zero); }
   /* full-size throw-away batches of one repeated short frag (it fails the
-     frag checks: no descriptors) through both slots */
+     frag checks: no descriptors) through every slot */
   std::vector<fd_ed25519_gpu_frag_t> fr( n );
   for( uint64_t i=0; i<n; i++ ) { fr[ i ].off = 0u; fr[ i ].sz = (uint32_t)(arena_sz < 64u ? arena_sz : 64u); }
-  std::vector<int8_t> status( 2u * n ); std::vector<uint64_t> tag( 2u * n );
+  std::vector<int8_t> status( (size_t)FD_VS_DEPTH * n ); std::vector<uint64_t> tag( (size_t)FD_VS_DEPTH * n );
   int err = FD_ED25519_GPU_OK, queued = 0;
-  for( int k=0; k<2 && !err; k++ ) {
+  for( int k=0; k<FD_VS_DEPTH && !err; k++ ) {
     err = fd_ed25519_gpu_frags_submit( st->ctx, arena, arena_sz, fr.data(), n, status.data() + k * n, tag.data() + k * n );
     queued += !err;
   }
@@ -506,13 +512,28 @@ fd_ed25519_gpu_stage_delete( fd_ed25519_gpu_stage_t * st ) {
   delete st;
 }
 
+/* Launch parsed batches (state 1) in submission order while the GPU side
+   takes them (it says BUSY when its queue of that kind is full, or while
+   batches of the other kind -- host vs device parse -- are pending). */
+static int
+vs_launch_ready( fd_ed25519_gpu_stage_t * st ) {
+  for( int j=0; j<st->pending; j++ ) {
+    vs_batch * b = &st->b[ (st->head + j) % FD_VS_DEPTH ];
+    if( b->state != 1 ) continue;
+    int err = vs_launch( st->ctx, b, st->threads );
+    if( err == FD_ED25519_GPU_ERR_BUSY ) return FD_ED25519_GPU_OK;
+    if( err ) return err;
+  }
+  return FD_ED25519_GPU_OK;
+}
+
 extern "C" int
 fd_ed25519_gpu_stage_submit( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, uint64_t arena_sz,
                              fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt, int8_t * result, uint64_t * sig ) {
   if( !st || (!frag && frag_cnt) || (frag_cnt && (!result || !sig)) || (!arena && arena_sz) ) return FD_ED25519_GPU_ERR_ARG;
   if( frag_cnt > st->max_frags ) return FD_ED25519_GPU_ERR_ARG;
-  if( st->pending == 2 ) return FD_ED25519_GPU_ERR_BUSY;
-  vs_batch * b = &st->b[ (st->head + st->pending) & 1 ];
+  if( st->pending == FD_VS_DEPTH ) return FD_ED25519_GPU_ERR_BUSY;
+  vs_batch * b = &st->b[ (st->head + st->pending) % FD_VS_DEPTH ];
   b->result = result; b->sig = sig;
   b->devp = st->devparse && frag_cnt && frag_cnt <= fd_ed25519_gpu_frags_cap( st->ctx );
   if( b->devp ) {
@@ -523,17 +544,9 @@ fd_ed25519_gpu_stage_submit( fd_ed25519_gpu_stage_t * st, uint8_t const * arena,
   }
   b->state = 1;
   st->pending++;
-  if( st->pending == 1 ) return vs_launch( st->ctx, b, st->threads );   /* the GPU is free: go */
-  /* Two device-parsed batches can both be queued: this one's frag span goes
-     to HBM on its own copy stream while the older one's kernels run (its
-     kernels follow them in order).  Otherwise it is launched when the
-     older batch's GPU work ends. */
-  vs_batch * ob = &st->b[ st->head ];
-  if( b->devp && ob->devp && ob->state >= 2 ) {
-    int err = vs_launch( st->ctx, b, st->threads );
-    return err == FD_ED25519_GPU_ERR_BUSY ? FD_ED25519_GPU_OK : err;
-  }
-  return FD_ED25519_GPU_OK;
+  /* straight to the GPU when its queue has room: with three batches in
+     flight the pipelined kernel runs one phase of each per launch */
+  return vs_launch_ready( st );
 }
 
 extern "C" int
@@ -544,24 +557,23 @@ fd_ed25519_gpu_stage_poll( fd_ed25519_gpu_stage_t * st, int block ) {
   if( b->state == 1 ) { int err = vs_launch( st->ctx, b, st->threads ); if( err ) return err; }
   if( b->state == 2 ) {
     for(;;) {
-      int r = b->devp ? fd_ed25519_gpu_frags_poll( st->ctx, 0 ) : fd_ed25519_gpu_poll( st->ctx );
+      int r = b->devp ? fd_ed25519_gpu_frags_poll( st->ctx, block ) : (block ? fd_ed25519_gpu_poll_block( st->ctx )
+                                                                                : fd_ed25519_gpu_poll( st->ctx ));
       if( r == FD_ED25519_GPU_OK ) break;
-      if( r != FD_ED25519_GPU_PENDING ) { b->state = 0; st->pending--; st->head ^= 1; return r; }
+      if( r != FD_ED25519_GPU_PENDING ) { b->state = 0; st->pending--; st->head = (st->head + 1) % FD_VS_DEPTH; return r; }
       if( !block ) return FD_ED25519_GPU_PENDING;
       std::this_thread::yield();
     }
     b->state = 3;
   }
-  /* the GPU is free: start the next batch before the host replays this one */
-  if( st->pending == 2 ) {
-    vs_batch * nb = &st->b[ st->head ^ 1 ];
-    if( nb->state == 1 ) { int err = vs_launch( st->ctx, nb, st->threads ); if( err ) return err; }
-  }
+  /* the GPU queue has room again: start the next parsed batches before the
+     host replays this one */
+  int err = vs_launch_ready( st );
   vs_replay( st->tc, b, st->threads );
   b->state = 0;
   st->pending--;
-  st->head ^= 1;
-  return FD_ED25519_GPU_OK;
+  st->head = (st->head + 1) % FD_VS_DEPTH;
+  return err;
 }
 
 extern "C" int

@@ -1,4 +1,5 @@
 """ctypes mirror of include/fd_ed25519_gpu.h (see package docstring)."""
+import collections
 import ctypes
 import os
 
@@ -67,6 +68,13 @@ def load_lib():
     lib.fd_ed25519_verify_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
     lib.fd_ed25519_gpu_submit.argtypes = [vp, vp, u64, vp, u64, vp]
     lib.fd_ed25519_gpu_poll.argtypes = [vp]
+    lib.fd_ed25519_gpu_poll_block.argtypes = [vp]
+    lib.fd_ed25519_gpu_pending.argtypes = [vp]
+    lib.fd_ed25519_gpu_pipe_status.argtypes = [vp, i32]
+    lib.fd_ed25519_gpu_test_ctab_stats.argtypes = [i32, vp, vp]
+    lib.fd_ed25519_gpu_launch_stats.argtypes = [vp, vp, vp]
+    lib.fd_ed25519_gpu_build_id.restype = ctypes.c_char_p
+    lib.fd_ed25519_gpu_build_id.argtypes = []
     lib.fd_ed25519_verify_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_pipe_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_pipe_flush_dev.argtypes = [vp, i32, vp]
@@ -79,6 +87,8 @@ def load_lib():
     lib.fd_ed25519_gpu_test_lattice.argtypes = [vp, vp, u64, vp]
     lib.fd_sha512_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
     lib.fd_sha512_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
+    lib.fd_sha256_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
+    lib.fd_sha256_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_tcache_new.restype = vp
     lib.fd_ed25519_gpu_tcache_new.argtypes = [u64, u64]
     lib.fd_ed25519_gpu_tcache_delete.argtypes = [vp]
@@ -112,6 +122,19 @@ def load_lib():
     lib.fd_ed25519_gpu_strerror.argtypes = [i32]
     _LIB = lib
     return lib
+
+
+def build_id():
+    """{"code": sha-256 prefix of the embedded code object, "git": describe of the built tree}"""
+    s = load_lib().fd_ed25519_gpu_build_id().decode()
+    return dict(kv.split("=", 1) for kv in s.split())
+
+
+def ctab_stats(dev=0):
+    """(live comb tables on HIP device dev, slots using it, tables built by this process)."""
+    refs, builds = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    live = load_lib().fd_ed25519_gpu_test_ctab_stats(dev, ctypes.byref(refs), ctypes.byref(builds))
+    return live, refs.value, builds.value
 
 
 def strerror(code):
@@ -205,6 +228,7 @@ class Ed25519Gpu:
 
     def __init__(self, device_mask=0, max_batch=1 << 18, codes=CODES_AVX512, devices=None):
         self.lib = load_lib()
+        self._keep = collections.deque()     # (arena, out) of the batches in flight
         if devices is not None:
             ids = (ctypes.c_int * len(devices))(*devices)
             self.ctx = self.lib.fd_ed25519_gpu_new_devs(ids, len(devices), max_batch)
@@ -243,16 +267,36 @@ class Ed25519Gpu:
         return out
 
     def submit(self, arena, arena_sz, desc, out):
-        self._keep = (arena, desc, out)
+        """fd_ed25519_gpu_submit: up to three batches in flight (the pipelined
+        kernel's depth); raises GpuError with ERR_BUSY on a fourth."""
         r = self.lib.fd_ed25519_gpu_submit(self.ctx, _ptr(arena), arena_sz, _ptr(desc), len(desc), _ptr(out))
         if r:
             raise GpuError("fd_ed25519_gpu_submit: %s (%d)" % (strerror(r), r))
+        self._keep.append((arena, out))
 
-    def poll(self):
-        r = self.lib.fd_ed25519_gpu_poll(self.ctx)
+    def poll(self, block=False):
+        """Completes the oldest submitted batch: True when its out is final."""
+        f = self.lib.fd_ed25519_gpu_poll_block if block else self.lib.fd_ed25519_gpu_poll
+        r = f(self.ctx)
         if r < 0:
+            if self._keep:
+                self._keep.popleft()
             raise GpuError("fd_ed25519_gpu_poll: %s (%d)" % (strerror(r), r))
+        if r == GPU_OK and self._keep:
+            self._keep.popleft()
         return r == GPU_OK
+
+    def launch_stats(self):
+        """(pipelined launches, one-shot launches) of this context so far."""
+        p, o = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self.lib.fd_ed25519_gpu_launch_stats(self.ctx, ctypes.byref(p), ctypes.byref(o))
+        return p.value, o.value
+
+    def pending(self):
+        return self.lib.fd_ed25519_gpu_pending(self.ctx)
+
+    def pipe_status(self, dev_idx=0):
+        return self.lib.fd_ed25519_gpu_pipe_status(self.ctx, dev_idx)
 
     def host_register(self, buf):
         """Page-lock a host array (e.g. a frag area) for every device of the context
@@ -376,8 +420,15 @@ class Ed25519Gpu:
             raise GpuError("fd_ed25519_gpu_shred_verify: %s (%d)" % (strerror(r), r))
         return out[:len(shreds)]
 
+    def sha256_batch(self, msgs):
+        """Batched SHA-256 of a list of byte strings (mirror of fd_sha256_batch_add per message)."""
+        return self._sha_batch(msgs, self.lib.fd_sha256_batch_gpu, 32, "fd_sha256_batch_gpu")
+
     def sha512_batch(self, msgs):
         """Batched SHA-512 of a list of byte strings (mirror of fd_sha512_batch_add per message)."""
+        return self._sha_batch(msgs, self.lib.fd_sha512_batch_gpu, 64, "fd_sha512_batch_gpu")
+
+    def _sha_batch(self, msgs, fn, dlen, name):
         msgs = list(msgs)
         total = sum(len(m) for m in msgs)
         arena = np.zeros(total + 16, np.uint8)
@@ -388,11 +439,11 @@ class Ed25519Gpu:
                 arena[off:off + len(m)] = np.frombuffer(m, np.uint8)
             desc[i] = (off, len(m))
             off += len(m)
-        out = np.zeros(64 * max(len(msgs), 1), np.uint8)
-        r = self.lib.fd_sha512_batch_gpu(self.ctx, _ptr(arena), total, _ptr(desc), len(msgs), _ptr(out))
+        out = np.zeros(dlen * max(len(msgs), 1), np.uint8)
+        r = fn(self.ctx, _ptr(arena), total, _ptr(desc), len(msgs), _ptr(out))
         if r:
-            raise GpuError("fd_sha512_batch_gpu: %s (%d)" % (strerror(r), r))
-        return [out[64 * i:64 * i + 64].tobytes() for i in range(len(msgs))]
+            raise GpuError("%s: %s (%d)" % (name, strerror(r), r))
+        return [out[dlen * i:dlen * i + dlen].tobytes() for i in range(len(msgs))]
 
     def sha512_batch_dev(self, d_arena, arena_sz, d_msg, msg_cnt, d_out, stream=0, dev_idx=0):
         r = self.lib.fd_sha512_batch_gpu_dev(self.ctx, dev_idx, d_arena, arena_sz, d_msg, msg_cnt, d_out, stream)

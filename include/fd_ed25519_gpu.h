@@ -71,9 +71,10 @@ typedef struct fd_ed25519_gpu fd_ed25519_gpu_t;
 /* Create a context over the GPUs in device_mask (bit i = HIP device i;
    0 = the calling thread's current device).  max_batch bounds the number of
    descriptors per call (device buffers are sized for it; larger calls are
-   split internally).  Each device slot holds a 5.9 GB fixed-base comb table
-   (built at creation, ~0.08 s) beside its max_batch-sized buffers.  Returns
-   NULL on failure (no device / OOM). */
+   split internally).  Every slot reads a 5.9 GB fixed-base comb table, ONE
+   per device per process, shared by all slots and contexts on it (built by
+   the first one, ~0.08 s; freed with the last) beside the slot's
+   max_batch-sized buffers.  Returns NULL on failure (no device / OOM). */
 fd_ed25519_gpu_t * fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch );
 /* Same over an explicit list of shard slots: slot j runs on HIP device
    dev_ids[j] with its own stream, tables and scratch; a device may appear
@@ -83,14 +84,22 @@ fd_ed25519_gpu_t * fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch 
 fd_ed25519_gpu_t * fd_ed25519_gpu_new_devs( int const * dev_ids, int ndev, uint64_t max_batch );
 void               fd_ed25519_gpu_delete( fd_ed25519_gpu_t * ctx );
 int                fd_ed25519_gpu_device_cnt( fd_ed25519_gpu_t const * ctx );
+/* Metrics: verify kernel launches so far by kind (pipelined; one-shot,
+   counting each chunk and each launch of the frags path). */
+int                fd_ed25519_gpu_launch_stats( fd_ed25519_gpu_t const * ctx, uint64_t * pipe_launches,
+                                                uint64_t * oneshot_launches );
 
 /* Select the error-code flavour (FD_ED25519_GPU_CODES_*). */
 int fd_ed25519_gpu_set_codes( fd_ed25519_gpu_t * ctx, int flavour );
 
-/* Synchronous batch verify over host memory: arena[0, arena_sz) and desc are
-   copied to the GPU(s), the batch is sharded contiguously over the context's
-   devices, and out_code[i] receives the code of desc[i].  Read interest in
-   arena/desc and write interest in out_code for the duration of the call. */
+/* Synchronous batch verify over host memory: the arena span the descriptors
+   touch and desc are copied to the GPU(s), the batch is sharded contiguously
+   over the context's devices, and out_code[i] receives the code of desc[i].
+   Read interest in arena/desc and write interest in out_code for the
+   duration of the call.  One batch alone gains nothing from the pipelined
+   kernel (its three phases would be three launches in a row), so this takes
+   the one-shot kernels; streams of batches go through submit / poll.
+   FD_ED25519_GPU_ERR_BUSY while async batches are pending. */
 int fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t *        ctx,
                                  uint8_t const *           arena,
                                  uint64_t                  arena_sz,
@@ -123,13 +132,25 @@ uint64_t fd_ed25519_gpu_keycache_cnt    ( fd_ed25519_gpu_t const * ctx );
 int      fd_ed25519_gpu_keycache_clear  ( fd_ed25519_gpu_t * ctx );
 
 /* Asynchronous pair (wiredancer-style push model, src/wiredancer/c/wd_f1.h:71-112):
-   submit enqueues the copies + kernels and returns; poll returns
-   FD_ED25519_GPU_PENDING until every device finished, then FD_ED25519_GPU_OK
-   (out_code valid) or an error.  One batch in flight per context.  The caller
-   keeps arena/desc/out_code alive until poll reports completion. */
+   submit copies the arena span the descriptors touch and the descriptors to
+   HBM on a copy stream and enqueues the kernels, and returns; up to three
+   batches are in flight (a fourth submit returns FD_ED25519_GPU_ERR_BUSY).
+   Batches of at most one wave per SIMD per device (256 x CUs signatures)
+   take the pipelined kernel (fd_ed25519_gpu_pipe_dev below): each launch runs
+   phase A of the new batch, B of the previous one and C of the one before,
+   so a batch's codes are final two submits later.  poll completes the
+   OLDEST batch: FD_ED25519_GPU_OK (its out_code valid), FD_ED25519_GPU_PENDING,
+   or an error.  A batch still short of its phase C (fewer than two submits
+   after it) gets drain launches: poll_block drains at once, poll only once
+   the device is idle (while launches run, more submits finish it for free).
+   The caller keeps a batch's arena and out_code until its poll reports
+   completion (desc is copied by submit).
+   FD_ED25519_GPU_ASYNC_PIPE=0 in the environment keeps the one-shot kernels. */
 int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
                            fd_ed25519_desc_t const * desc, uint64_t desc_cnt, int8_t * out_code );
 int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * ctx );
+int fd_ed25519_gpu_poll_block( fd_ed25519_gpu_t * ctx );
+int fd_ed25519_gpu_pending( fd_ed25519_gpu_t const * ctx );   /* batches submitted, not yet polled */
 
 /* Device-resident entry point (no host copies): d_arena / d_desc / d_out are
    device pointers on the context's shard slot dev_idx, stream is a
@@ -170,6 +191,11 @@ int fd_ed25519_gpu_pipe_dev( fd_ed25519_gpu_t * ctx, int dev_idx,
                              int8_t * d_out, void * stream );
 /* Enqueues the drain steps that finish every pending batch (no-op if none). */
 int fd_ed25519_gpu_pipe_flush_dev( fd_ed25519_gpu_t * ctx, int dev_idx, void * stream );
+/* After the caller's stream has completed the launches: FD_ED25519_GPU_OK, or
+   FD_ED25519_GPU_ERR_LAUNCH if any pipelined launch on the slot failed its
+   internal consistency check (a phase-A workgroup wait that expired; its
+   codes must not be used).  pipe_dev / submit / poll report it too. */
+int fd_ed25519_gpu_pipe_status( fd_ed25519_gpu_t * ctx, int dev_idx );
 
 /* Single-signature and single-message-batch drop-ins (host memory, synchronous).
    *out receives the verify code exactly as fd_ed25519_verify /
@@ -194,6 +220,11 @@ int64_t fd_ed25519_gpu_txn_reduce( int8_t const * out_code, fd_ed25519_desc_t co
 
 char const * fd_ed25519_gpu_strerror( int err );
 
+/* "code=<first 16 hex digits of the SHA-256 of the embedded gfx950 code
+   object> git=<git describe of the tree it was built from>": profiles
+   (profiles/rNN/) record it, so a measurement can be matched to a build. */
+char const * fd_ed25519_gpu_build_id( void );
+
 /* Batched SHA-512 (replaces fd_sha512_batch_init/_add/_fini,
    src/ballet/sha512/fd_sha512.h:223-408, i.e. fd_sha512_hash per message,
    fd_sha512.c:399): message i is arena[msg[i].off, msg[i].off+msg[i].sz),
@@ -211,6 +242,16 @@ int fd_sha512_batch_gpu( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t
 /* Device-resident variant (enqueue only; d_arena readable up to
    align_up(arena_sz,4)+8 bytes, d_out 64*msg_cnt bytes). */
 int fd_sha512_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx, uint8_t const * d_arena, uint64_t arena_sz,
+                             fd_sha512_gpu_msg_t const * d_msg, uint64_t msg_cnt, uint8_t * d_out, void * stream );
+
+/* Batched SHA-256, same shape (replaces fd_sha256_hash and the
+   fd_sha256_batch_* API, src/ballet/sha256/fd_sha256.h): message i is
+   arena[msg[i].off, msg[i].off+msg[i].sz), its 32-byte digest goes to
+   out_hash[32 i, 32 i + 32).  The device kernel is also the shred Merkle
+   path's hash (fd_ed25519_gpu_shred_verify). */
+int fd_sha256_batch_gpu( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                         fd_sha512_gpu_msg_t const * msg, uint64_t msg_cnt, uint8_t * out_hash );
+int fd_sha256_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx, uint8_t const * d_arena, uint64_t arena_sz,
                              fd_sha512_gpu_msg_t const * d_msg, uint64_t msg_cnt, uint8_t * d_out, void * stream );
 
 /* ---- Verify stage ---------------------
@@ -285,10 +326,11 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
    poll completes the OLDEST outstanding batch -- when its GPU work is done it
    starts the next batch's GPU work, then replays the tcache steps for the
    completed batch and fills its result / sig arrays -- and returns
-   FD_ED25519_GPU_OK, or FD_ED25519_GPU_PENDING (block == 0 only).  At most two
-   batches are outstanding (submit returns FD_ED25519_GPU_ERR_BUSY on a
-   third), so the host parse of batch k+1 and the replay of batch k overlap
-   the GPU.  Batches complete strictly in submission order, which keeps the
+   FD_ED25519_GPU_OK, or FD_ED25519_GPU_PENDING (block == 0 only).  At most
+   three batches are outstanding (submit returns FD_ED25519_GPU_ERR_BUSY on a
+   fourth): each goes to the GPU at submit, so the pipelined kernel runs one
+   phase of each per launch, and the host parse of batch k+1 and the replay
+   of batch k overlap the GPU.  Batches complete strictly in submission order, which keeps the
    tile's frag order for the tcache.  The frag bytes and the result / sig
    arrays of a batch must stay valid until its poll returns OK.  The stage
    uses ctx's async pair: no other submit on ctx while batches are pending. */
@@ -451,6 +493,10 @@ int fd_ed25519_gpu_shred_verify( fd_ed25519_gpu_t * ctx, uint8_t * arena, uint64
 
 /* SHA-256 (FIPS 180-4) of msg, host; the Merkle hashing above uses it. */
 void fd_ed25519_gpu_sha256( uint8_t const * msg, uint64_t sz, uint8_t out[ 32 ] );
+
+/* Test hook: comb tables alive on HIP device dev (0 or 1), *refs = the slots
+   using it, *builds = tables this process has built so far. */
+int fd_ed25519_gpu_test_ctab_stats( int dev, uint64_t * refs, uint64_t * builds );
 
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE

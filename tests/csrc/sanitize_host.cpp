@@ -58,19 +58,38 @@ int fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t * ctx, uint8_t const * arena, 
   (void)ctx;
   return stand_in_verify( arena, arena_sz, desc, n, out );
 }
+/* the async pair's queue discipline: up to three batches in flight, oldest completes first */
 int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
                            fd_ed25519_desc_t const * desc, uint64_t n, int8_t * out ) {
-  if( ctx->pend ) return FD_ED25519_GPU_ERR_BUSY;
+  if( ctx->pend >= 3 ) return FD_ED25519_GPU_ERR_BUSY;
   int e = stand_in_verify( arena, arena_sz, desc, n, out );
-  if( !e ) ctx->pend = 1;
+  if( !e ) ctx->pend++;
   return e;
 }
-int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * ctx ) { ctx->pend = 0; return FD_ED25519_GPU_OK; }
+int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * ctx ) { if( ctx->pend ) ctx->pend--; return FD_ED25519_GPU_OK; }
+int fd_ed25519_gpu_poll_block( fd_ed25519_gpu_t * ctx ) { return fd_ed25519_gpu_poll( ctx ); }
 uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx ) { (void)ctx; return 0u; }   /* host parse only */
 int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n ) { (void)ctx; (void)n; return FD_ED25519_GPU_ERR_ARG; }
 int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t *, uint8_t const *, uint64_t, fd_ed25519_gpu_frag_t const *, uint64_t,
                                  int8_t *, uint64_t * ) { return FD_ED25519_GPU_ERR_ARG; }
 int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t *, int ) { return FD_ED25519_GPU_OK; }
+/* the shred path's GPU half: reads every byte the root kernel would (leaf,
+   proof nodes), writes a stand-in root where the kernel writes the real one */
+typedef struct { uint32_t leaf_off, leaf_len, proof_off, out_off; uint16_t depth, idx; } stand_in_job_t;
+int fd_ed25519_gpu_merkle_verify( fd_ed25519_gpu_t *, uint8_t * arena, uint64_t arena_sz, uint64_t aux_off,
+                                  uint64_t aux_sz, stand_in_job_t const * job, fd_ed25519_desc_t const * desc, uint64_t n,
+                                  int8_t * code ) {
+  for( uint64_t i=0; i<n; i++ ) {
+    stand_in_job_t const & j = job[ i ];
+    if( (uint64_t)j.leaf_off + j.leaf_len > arena_sz || (uint64_t)j.proof_off + 20u * j.depth > arena_sz ||
+        j.out_off < aux_off || (uint64_t)j.out_off + 32u > aux_off + aux_sz ) return FD_ED25519_GPU_ERR_ARG;
+    uint32_t h = 2166136261u;
+    for( uint32_t k=0; k<j.leaf_len; k++ ) h = (h ^ arena[ j.leaf_off + k ]) * 16777619u;
+    for( uint32_t k=0; k<20u * j.depth; k++ ) h = (h ^ arena[ j.proof_off + k ]) * 16777619u;
+    for( uint32_t k=0; k<32; k++ ) arena[ j.out_off + k ] = (uint8_t)(h >> (k & 24));
+  }
+  return stand_in_verify( arena, arena_sz, desc, n, code );
+}
 }
 
 /* ---- random inputs ---- */

@@ -57,6 +57,8 @@ txn_batches.bin record:
   u32 n, u32 msg_sz, i8 code_avx512, i8 code_ref, u16 0, u8 sigs[64n], u8 pubs[32n], u8 msg[msg_sz]
 sha512_kat.bin record:
   u32 msg_sz, u8 digest[64], u8 msg[msg_sz]
+sha256_kat.bin record (fd_sha256_test_vector.c + CAVP SHA256{Short,Long}Msg.rsp, every 4th):
+  u32 msg_sz, u8 digest[32], u8 msg[msg_sz]
 shreds.bin record:
   u32 tag, u32 sz, i32 result (verify code, or -101..-106 as oracle/ref_shred.c), u8 root[32],
   u8 leader[32], u8 shred[sz]
@@ -536,12 +538,36 @@ def gen_sha512(vecs):
     return out
 
 
+def gen_sha256(vecs):
+    out = []
+    for set_id, tc_id, ok, msg, sig, pub in vecs:
+        if set_id == 4:
+            out.append(struct.pack("<I", len(msg)) + sig[:32] + msg)
+    # NIST CAVP (src/ballet/sha256/cavp/SHA256{Short,Long}Msg.rsp), every 4th record
+    for fname in ("SHA256ShortMsg.rsp", "SHA256LongMsg.rsp"):
+        path = os.path.join(REF_SRC, "ballet/sha256/cavp", fname)
+        ln = None; msg = None; k = 0
+        for line in open(path):
+            line = line.strip()
+            if line.startswith("Len ="):
+                ln = int(line.split("=")[1])
+            elif line.startswith("Msg ="):
+                msg = bytes.fromhex(line.split("=")[1].strip())[: ln // 8]
+            elif line.startswith("MD ="):
+                md = bytes.fromhex(line.split("=")[1].strip())
+                if k % 4 == 0:
+                    out.append(struct.pack("<I", len(msg)) + md + msg)
+                k += 1
+    return out
+
+
 def main():
     global LIBS
     LIBS = load_libs()
     vecs = extract_reference_vectors()
     gens = {"vectors_ref.bin": lambda: gen_vectors_ref(vecs), "synthetic.bin": gen_synthetic,
             "txn_batches.bin": gen_txn_batches, "sha512_kat.bin": lambda: gen_sha512(vecs),
+            "sha256_kat.bin": lambda: gen_sha256(vecs),
             "cctv_batches.bin": lambda: gen_cctv_batches(vecs), "fuzz_seeds.bin": gen_fuzz_seeds,
             "gossip.bin": gen_gossip, "shreds.bin": gen_shreds}
     only = sys.argv[1:] or list(gens)

@@ -32,12 +32,14 @@ def read_txns(name="txn_batches.bin"):
     return out
 
 
-def read_sha(name="sha512_kat.bin"):
+def read_sha(name="sha512_kat.bin", dlen=None):
+    """[(msg, digest)] of a KAT file (digest 64 B for sha512_kat.bin, 32 B for sha256_kat.bin)."""
+    dlen = dlen or (32 if "256" in name else 64)
     data = open(os.path.join(GOLDEN, name), "rb").read()
     out, off = [], 0
     while off < len(data):
         (sz,) = struct.unpack_from("<I", data, off); off += 4
-        md = data[off:off + 64]; off += 64
+        md = data[off:off + dlen]; off += dlen
         out.append((data[off:off + sz], md)); off += sz
     return out
 

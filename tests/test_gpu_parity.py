@@ -242,6 +242,27 @@ def test_sha512_batch_kats_and_random(gpu):
         assert g == hashlib.sha512(m).digest(), (len(m),)
 
 
+def test_sha256_batch_kats_and_random(gpu):
+    """Batched SHA-256 kernel (fd_sha256_hash / fd_sha256_batch replacement,
+    the shred Merkle path's hash) against the reference's SHA-256 KATs
+    (fd_sha256_test_vector.c + CAVP, tests/golden/sha256_kat.bin) and hashlib
+    on random lengths 0..3000 at arbitrary byte alignments, and the lengths
+    around the padding boundary."""
+    import hashlib
+    from golden_io import read_sha
+    kats = read_sha("sha256_kat.bin")
+    assert len(kats) == 77
+    got = gpu.sha256_batch([m for m, _ in kats])
+    for (m, h), g in zip(kats, got):
+        assert g == h, (len(m),)
+    rng = np.random.default_rng(22)
+    msgs = [rng.bytes(int(rng.integers(0, 3001))) for _ in range(4000)]
+    msgs += [bytes(n) for n in (0, 1, 54, 55, 56, 57, 63, 64, 65, 118, 119, 120, 127, 128, 129)]
+    got = gpu.sha256_batch(msgs)
+    for m, g in zip(msgs, got):
+        assert g == hashlib.sha256(m).digest(), (len(m),)
+
+
 def test_pair_and_single_lane_kernels_agree(gpu):
     """Batches of at most one 256-signature workgroup per CU take the pair
     kernel (two lanes per signature for the decodes), larger ones the

@@ -85,3 +85,56 @@ def test_shred_verify_gpu(gpu):
     out = gpu.shred_verify(arena, len(arena), aux_off, aux_cap, spans, keys)
     exp = np.array([STATUS.get(r["result"], r["result"]) for r in RECS], np.int32)
     assert np.array_equal(out, exp), [(RECS[j]["tag"], out[j], exp[j]) for j in np.nonzero(out != exp)[0][:10]]
+
+
+@pytest.mark.gpu
+def test_shred_roots_on_gpu_equal_reference_roots(gpu):
+    """The default shred_verify hashes the Merkle roots on the GPU
+    (fd_shred_root_kernel) and copies them into aux: the same 32 bytes the
+    reference bmtree gives; the host-hash path (FD_ED25519_GPU_SHRED_HOST_HASH=1)
+    gives the same codes and roots."""
+    import os
+    arena, spans, keys, aux_off, aux_cap = _arena()
+    desc, sd = fa.shred_walk(arena.copy(), len(arena), aux_off, aux_cap, spans, keys)   # descriptor order
+    a1 = arena.copy()
+    out = gpu.shred_verify(a1, len(a1), aux_off, aux_cap, spans, keys)
+    b = a1.tobytes()
+    nver = 0
+    for j, r in enumerate(RECS):
+        if r["result"] > -100:
+            d = desc[sd[j]]
+            assert b[d["msg_off"]:d["msg_off"] + 32] == r["root"], r["tag"]
+            nver += 1
+    assert nver >= 480
+    a2 = arena.copy()
+    os.environ["FD_ED25519_GPU_SHRED_HOST_HASH"] = "1"
+    try:
+        out2 = gpu.shred_verify(a2, len(a2), aux_off, aux_cap, spans, keys)
+    finally:
+        del os.environ["FD_ED25519_GPU_SHRED_HOST_HASH"]
+    assert np.array_equal(out, out2)
+    assert np.array_equal(a1, a2)
+
+
+@pytest.mark.gpu
+def test_shred_roots_many(gpu, oracle):
+    """The capture's shreds tiled 64 times (30K shreds, different arena
+    offsets): every root equals the host walk's, every code the fixture's."""
+    reps = 64
+    blob, spans, keys, want = bytearray(), [], [], []
+    for t in range(reps):
+        for r in RECS:
+            keys.append(len(blob)); blob += r["leader"]
+            blob += b"\x33" * ((t + len(blob)) % 5)
+            spans.append((len(blob), len(r["shred"]))); blob += r["shred"]
+            want.append(STATUS.get(r["result"], r["result"]))
+    aux_off = len(blob)
+    n = len(spans)
+    arena = np.zeros(aux_off + 32 * n, np.uint8)
+    arena[:aux_off] = np.frombuffer(bytes(blob), np.uint8)
+    spans = np.array(spans, fa.SPAN_DTYPE); keys = np.array(keys, np.uint32)
+    host = arena.copy()
+    fa.shred_walk(host, len(host), aux_off, 32 * n, spans, keys)
+    out = gpu.shred_verify(arena, len(arena), aux_off, 32 * n, spans, keys)
+    assert np.array_equal(out, np.array(want, np.int32))
+    assert np.array_equal(arena, host)

@@ -95,38 +95,50 @@ def main():
         times.append(time.perf_counter() - t1)
     dt = float(np.mean(times))
     # the asynchronous stage with the frags parsed on the GPU: --async-batch
-    # frags per batch, two batches in flight, over the same stream
+    # frags per batch, three batches in flight (the pipelined kernel: one
+    # phase of each per launch), over the same stream; and the same with the
+    # one-shot kernels (FD_ED25519_GPU_ASYNC_PIPE=0) for the A/B
     ab = args.async_batch
-    big = fa.Ed25519Gpu(device_mask=1, max_batch=16 * ab)
-    ast = fa.AsyncStage(big, fa.TCache(), ab, threads=8, device_parse=True)
-    res_a = np.zeros(len(frags), np.int8); sig_a = np.zeros(len(frags), np.uint64)
     fr = np.ascontiguousarray(frags)
 
-    def run_async():
-        ast.tcache.reset()
-        i = 0
-        while i < len(fr) or ast.pending():
-            if i < len(fr) and ast.pending() < 2:
-                j = min(len(fr), i + ab)
-                ast.submit(arena, len(arena), fr[i:j], res_a[i:j], sig_a[i:j])
-                i = j
-            else:
-                ast.poll(True)
-    def timed():
-        run_async()
-        t = []
-        for _ in range(args.steps):
-            t1 = time.perf_counter(); run_async(); t.append(time.perf_counter() - t1)
-        return float(np.mean(t))
-    dt_a = timed()
-    res_pageable = res_a.copy()
-    # the same with the frag area page-locked (a tile's dcache workspace is
-    # registered once: fd_ed25519_gpu_host_register)
-    big.host_register(arena)
-    dt_r = timed()
-    big.host_unregister(arena)
-    assert np.array_equal(res_a, res_pageable)
-    ast.close(); big.close()
+    def measure(pipe):
+        os.environ["FD_ED25519_GPU_ASYNC_PIPE"] = "1" if pipe else "0"
+        big = fa.Ed25519Gpu(device_mask=1, max_batch=16 * ab)
+        ast = fa.AsyncStage(big, fa.TCache(), ab, threads=8, device_parse=True)
+        res_a = np.zeros(len(frags), np.int8); sig_a = np.zeros(len(frags), np.uint64)
+
+        def run_async():
+            ast.tcache.reset()
+            i = 0
+            while i < len(fr) or ast.pending():
+                if i < len(fr) and ast.pending() < 3:
+                    j = min(len(fr), i + ab)
+                    ast.submit(arena, len(arena), fr[i:j], res_a[i:j], sig_a[i:j])
+                    i = j
+                else:
+                    ast.poll(True)
+
+        def timed():
+            run_async()
+            t = []
+            for _ in range(args.steps):
+                t1 = time.perf_counter(); run_async(); t.append(time.perf_counter() - t1)
+            return float(np.mean(t))
+        dt_a = timed()
+        res_pageable = res_a.copy()
+        # the same with the frag area page-locked (a tile's dcache workspace is
+        # registered once: fd_ed25519_gpu_host_register)
+        big.host_register(arena)
+        dt_r = timed()
+        big.host_unregister(arena)
+        assert np.array_equal(res_a, res_pageable)
+        launches = big.launch_stats()
+        ast.close(); big.close()
+        os.environ.pop("FD_ED25519_GPU_ASYNC_PIPE", None)
+        return dt_a, dt_r, res_a, launches
+    dt_a, dt_r, res_a, launches = measure(True)
+    dt_o, dt_or, res_o, launches_o = measure(False)
+    assert np.array_equal(res_a, res_o)
     line = {"metric": "verify-stage frags/sec (fd_ed25519_gpu_verify_frags, host frags)",
             "value": args.frags / dt, "unit": "frags/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt * 1e3, "higher_is_better": True, "dtype": "u32 limbs / u8 bytes",
@@ -135,8 +147,15 @@ def main():
                        "arena_bytes": int(len(arena))},
             "sigs_per_s": n_sigs / dt, "host_parse_ms": parse_ms, "results": hist, "gen_s": gen_s,
             "async_device_parse": {"frags_per_s": args.frags / dt_a, "ms": dt_a * 1e3, "batch": ab,
+                                   "in_flight": 3, "kernel": "pipelined", "launches_pipe_oneshot": launches,
                                    "registered_frags_per_s": args.frags / dt_r, "registered_ms": dt_r * 1e3,
+                                   "sigs_per_s": n_sigs / dt_a, "registered_sigs_per_s": n_sigs / dt_r,
                                    "results": {int(k): int(v) for k, v in zip(*np.unique(res_a, return_counts=True))}},
+            "async_device_parse_oneshot": {"frags_per_s": args.frags / dt_o, "ms": dt_o * 1e3,
+                                           "registered_frags_per_s": args.frags / dt_or,
+                                           "sigs_per_s": n_sigs / dt_o, "registered_sigs_per_s": n_sigs / dt_or,
+                                           "launches_pipe_oneshot": launches_o,
+                                           "note": "FD_ED25519_GPU_ASYNC_PIPE=0: the same stage on the one-shot kernels"},
             "cpu_baseline": None if args.no_cpu else cpu_baseline(arena, frags)}
     print(json.dumps(line), flush=True)
     stage.close()

@@ -1,0 +1,13 @@
+#!/bin/bash
+# r03 session: full GPU suite, the driver-form bench, and the verify-stage
+# A/B (pipelined vs one-shot async stage).  Each step time-limited; stop at
+# the first failure.
+set -e
+mkdir -p gpurun_out
+T=${TAG:-r03b}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1 || { tail -60 gpurun_out/gpu_tests_$T.log; exit 1; }
+tail -3 gpurun_out/gpu_tests_$T.log
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { tail -20 gpurun_out/bench_$T.err; exit 1; }
+cat gpurun_out/bench_$T.json
+timeout -k 10 400 python3 tools/bench_verify_stage.py --frags 262144 --no-cpu > gpurun_out/stage_$T.json 2> gpurun_out/stage_$T.err || { tail -20 gpurun_out/stage_$T.err; exit 1; }
+cat gpurun_out/stage_$T.json

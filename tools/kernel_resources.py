@@ -9,7 +9,7 @@ SQ counters of profiles/r02/pmc_sq.json it adds the achieved mean waves per SIMD
 of the profiled verify launch (SQ_WAVE_CYCLES counts quad-cycles).
 
   KR_ASM=<kern.opt.s> python3 tools/kernel_resources.py [out.json]   (default asm: the prod build,
-                                                                   default out: profiles/r02/kernel_resources.json)
+                                                                   default out: /dev/stdout only; pass a path to write one)
 """
 import json
 import os
@@ -48,15 +48,20 @@ def limits(k):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r02", "kernel_resources.json")
-    if not out.endswith(".json"):
+    out = sys.argv[1] if len(sys.argv) > 1 else None
+    if out is not None and not out.endswith(".json"):
         sys.exit("kernel_resources.py: the argument is the OUTPUT .json (the asm comes from KR_ASM or the prod build)")
-    rep = {"source": os.path.relpath(ASM, REPO), "model": "gfx950: 512 VGPRs/SIMD lane, granule 8; "
+    bid = os.path.join(os.path.dirname(ASM), "fd_build_id.h")
+    build = None
+    if os.path.exists(bid):
+        t = open(bid).read().split('"')[1]
+        build = dict(kv.split("=", 1) for kv in t.split())
+    rep = {"source": os.path.relpath(ASM, REPO), "build": build, "model": "gfx950: 512 VGPRs/SIMD lane, granule 8; "
            "160 KB LDS/CU; 8 waves/SIMD; 4 SIMDs/CU; 256 CUs", "kernels": {}}
     for k in metadata(ASM):
         rep["kernels"][k[".name"]] = limits(k)
-    pmc = os.path.join(REPO, "profiles", "r02", "pmc_sq.json")
-    if os.path.exists(pmc):
+    pmc = os.environ.get("KR_PMC", "")          # a pmc_sq.json for the achieved waves per SIMD
+    if pmc and os.path.exists(pmc):
         p = json.load(open(pmc))
         cyc = p["dur_ns"] * 1e-9 * p["effective_clock_ghz"] * 1e9
         rep["achieved"] = {
@@ -65,7 +70,8 @@ def main():
             "note": "SQ_WAVE_CYCLES (quad-cycles x4) / (launch cycles at the GRBM clock x 1,024 SIMDs); "
                     "config 2 pipelined = three waves per SIMD (phases A, B, C of three batches)",
         }
-    json.dump(rep, open(out, "w"), indent=1)
+    if out:
+        json.dump(rep, open(out, "w"), indent=1)
     print(json.dumps(rep, indent=1))
 
 

@@ -3,12 +3,13 @@
 # has its own time limit; the script stops at the first failure.
 #   tools/profile.sh <tag>   -> gpurun_out/prof_<tag>/...
 set -e
-TAG=${1:-r02}
+TAG=${1:-r03}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 BENCH="bench.py --no-cpu"
 timeout -k 10 240 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 240 python3 bench.py --steps 20 --warmup 5 > $OUT/bench_driver_form.json 2> $OUT/bench_driver_form.err
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $BENCH > $OUT/kt_bench.json 2> $OUT/kt.err
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2> $OUT/pmc_fetch.err
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 bench.py --steps 3 --warmup 1 --no-cpu > /dev/null 2> $OUT/pmc_write.err

@@ -4,6 +4,8 @@
 
   kernel_stats.csv    rocprofv3 --kernel-trace --stats summary (verbatim)
   bench.json          the bench.py line of the same tree (un-profiled run)
+  bench_driver_form.json  the same in the driver's form (--steps 20 --warmup 5), if run
+  build.json          the library's build id (code-object hash + git) every file here is keyed to
   pmc_traffic.json    HBM bytes per verify-kernel launch from separate
                       FETCH_SIZE / WRITE_SIZE passes, with the gfx950
                       correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE x 2
@@ -50,6 +52,13 @@ def main():
     bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
     json.dump(bench, open(os.path.join(dst, "bench.json"), "w"))
     n = bench["config"]["batch_per_gpu"]
+    build = bench.get("build")
+    drv = os.path.join(src, "bench_driver_form.json")
+    if os.path.exists(drv):
+        d = json.loads(open(drv).read().strip().splitlines()[-1])
+        assert d.get("build") == build, "driver-form bench ran a different build"
+        json.dump(d, open(os.path.join(dst, "bench_driver_form.json"), "w"))
+    json.dump(build, open(os.path.join(dst, "build.json"), "w"))
 
     fe = pmc(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv"))
     wr = pmc(os.path.join(src, "pmc_write", "pmc_counter_collection.csv"))
@@ -57,6 +66,7 @@ def main():
     write_kb = statistics.median(d["WRITE_SIZE"] for d in wr)
     hbm = (2.0 * fetch_kb + write_kb) * 1024.0
     traffic = {
+        "build": build,
         "batch": n, "kernel": verify_kernel(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv")),
         "launches": len(fe),
         "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
@@ -76,6 +86,7 @@ def main():
     waves = sq["SQ_WAVES"]
     out = {k: v for k, v in sq.items()}
     out.update({
+        "build": build,
         "kernel": verify_kernel(os.path.join(src, "pmc_sq", "pmc_counter_collection.csv")),
         "valu_instr_per_wave": sq["SQ_INSTS_VALU"] / waves,
         "valu_instr_per_64_sigs": sq["SQ_INSTS_VALU"] / (n / 64.0),
