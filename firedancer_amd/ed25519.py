@@ -106,6 +106,10 @@ def load_lib():
     lib.fd_ed25519_gpu_gossip_walk.restype = ctypes.c_int64
     lib.fd_ed25519_gpu_gossip_walk.argtypes = [vp, u64, u64, u64, vp, u64, vp, vp, u64, vp]
     lib.fd_ed25519_gpu_gossip_verify.argtypes = [vp, vp, u64, u64, u64, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_gossip_walk_crds.restype = ctypes.c_int64
+    lib.fd_ed25519_gpu_gossip_walk_crds.argtypes = [vp, u64, u64, u64, vp, u64, vp, vp, u64, vp, vp]
+    lib.fd_ed25519_gpu_gossip_verify_crds.restype = ctypes.c_int64
+    lib.fd_ed25519_gpu_gossip_verify_crds.argtypes = [vp, vp, u64, u64, u64, vp, u64, vp, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_shred_walk.restype = ctypes.c_int64
     lib.fd_ed25519_gpu_shred_walk.argtypes = [vp, u64, u64, u64, vp, vp, u64, vp, u64, vp]
     lib.fd_ed25519_gpu_shred_verify.argtypes = [vp, vp, u64, u64, u64, vp, vp, u64, vp]
@@ -168,7 +172,12 @@ def pack_batch(records):
     return arena, desc, total
 
 
-GOSSIP_CORRUPT, GOSSIP_UNSIGNED, GOSSIP_NOT_MINE, GOSSIP_CRDS = -110, -111, -112, -113
+GOSSIP_CORRUPT, GOSSIP_UNSIGNED, GOSSIP_NOT_MINE, GOSSIP_CRDS, GOSSIP_NO_VALUES = -110, -111, -112, -113, -114
+
+
+def _gossip_desc_cap(pkts):
+    """every signed value holds a 64-byte signature: a packet has at most sz / 64 + 1"""
+    return int(np.sum(pkts["sz"] // 64)) + len(pkts) + 1
 
 
 def gossip_walk(arena, arena_sz, aux_off, aux_cap, pkts, self_pubkey=None):
@@ -184,6 +193,24 @@ def gossip_walk(arena, arena_sz, aux_off, aux_cap, pkts, self_pubkey=None):
     if nd < 0:
         raise GpuError("fd_ed25519_gpu_gossip_walk: %s (%d)" % (strerror(int(nd)), nd))
     return desc[:nd], pd[:n]
+
+
+def gossip_walk_crds(arena, arena_sz, aux_off, aux_cap, pkts, self_pubkey=None):
+    """fd_ed25519_gpu_gossip_walk_crds (host, no GPU): CRDS values walked too
+    -> (desc, pkt_desc, pkt_cnt)."""
+    lib = load_lib()
+    pkts = np.ascontiguousarray(pkts, dtype=SPAN_DTYPE)
+    n = len(pkts)
+    cap = _gossip_desc_cap(pkts)
+    desc = np.zeros(cap, DESC_DTYPE)
+    pd = np.zeros(max(n, 1), np.int64)
+    pc = np.zeros(max(n, 1), np.uint32)
+    me = None if self_pubkey is None else ctypes.c_char_p(bytes(self_pubkey))
+    nd = lib.fd_ed25519_gpu_gossip_walk_crds(_ptr(arena), arena_sz, aux_off, aux_cap, _ptr(pkts), n, me,
+                                             _ptr(desc), cap, _ptr(pd), _ptr(pc))
+    if nd < 0:
+        raise GpuError("fd_ed25519_gpu_gossip_walk_crds: %s (%d)" % (strerror(int(nd)), nd))
+    return desc[:nd], pd[:n], pc[:n]
 
 
 SHRED_PARSE, SHRED_ZERO_SIG, SHRED_COUNTS, SHRED_INDEX, SHRED_DEPTH, SHRED_PROOF = -120, -121, -122, -123, -124, -125
@@ -406,6 +433,24 @@ class Ed25519Gpu:
         if r:
             raise GpuError("fd_ed25519_gpu_gossip_verify: %s (%d)" % (strerror(r), r))
         return out[:len(pkts)]
+
+    def gossip_verify_crds(self, arena, arena_sz, aux_off, aux_cap, pkts, self_pubkey=None):
+        """gossip_verify with the CRDS values of pull responses / pushes too
+        -> (int8 code per descriptor, pkt_desc, pkt_cnt): packet j's values
+        are codes[pkt_desc[j]:pkt_desc[j] + pkt_cnt[j]] in value order (the
+        others this node's own), or pkt_desc[j] is a GOSSIP_* status."""
+        pkts = np.ascontiguousarray(pkts, dtype=SPAN_DTYPE)
+        n = len(pkts)
+        cap = _gossip_desc_cap(pkts)
+        code = np.zeros(cap, np.int8)
+        pd = np.zeros(max(n, 1), np.int64)
+        pc = np.zeros(max(n, 1), np.uint32)
+        me = None if self_pubkey is None else ctypes.c_char_p(bytes(self_pubkey))
+        r = self.lib.fd_ed25519_gpu_gossip_verify_crds(self.ctx, _ptr(arena), arena_sz, aux_off, aux_cap, _ptr(pkts),
+                                                       n, me, _ptr(code), cap, _ptr(pd), _ptr(pc))
+        if r < 0:
+            raise GpuError("fd_ed25519_gpu_gossip_verify_crds: %s (%d)" % (strerror(int(r)), r))
+        return code[:r], pd[:n], pc[:n]
 
     def shred_verify(self, arena, arena_sz, aux_off, aux_cap, shreds, key_off):
         """Shreds (SPAN_DTYPE spans of arena) with their leaders' keys at

@@ -440,6 +440,7 @@ int64_t fd_ed25519_gpu_precompile_walk( uint8_t const * arena, uint64_t arena_sz
 #define FD_ED25519_GPU_GOSSIP_UNSIGNED  (-111)
 #define FD_ED25519_GPU_GOSSIP_NOT_MINE  (-112)
 #define FD_ED25519_GPU_GOSSIP_CRDS      (-113)
+#define FD_ED25519_GPU_GOSSIP_NO_VALUES (-114)   /* a CRDS packet whose values are all this node's own */
 
 /* Host, no GPU.  pkt_desc[j] = the index of packet j's descriptor in desc
    (descriptor txn_idx = j mod 2^16) or one of the statuses above.  aux must
@@ -456,6 +457,31 @@ int64_t fd_ed25519_gpu_gossip_walk( uint8_t * arena, uint64_t arena_sz, uint64_t
 int fd_ed25519_gpu_gossip_verify( fd_ed25519_gpu_t * ctx, uint8_t * arena, uint64_t arena_sz, uint64_t aux_off,
                                   uint64_t aux_cap, fd_ed25519_gpu_span_t const * pkt, uint64_t n,
                                   uint8_t const * self, int * out );
+
+/* The same walk with the CRDS values of pull responses and pushes walked too
+   (fd_gossip_recv_crds_value, fd_gossip.c:830-900): the packet is decoded
+   whole with the reference decoder's rules (else CORRUPT), and every value
+   whose key -- its own from / id by variant, or the message's pubkey for
+   contact-info v2 -- is not `self` gets one descriptor: sig = the value's
+   signature, key in the packet, msg = the value's data re-encoded the way
+   the reference encoder writes it (fd_crds_data_encode; not always the
+   received bytes: option tags become 0 / 1, a varint wallclock minimal, the
+   varint-u16 fields of the v2 contact info fixed u16) into aux.  A value
+   whose encoding exceeds the node's 1500-byte buffer (the reference
+   FD_LOG_ERRs) is skipped.  pkt_desc[j] = packet j's first descriptor (its
+   pkt_cnt[j] descriptors are contiguous, in value order, txn_idx = j mod
+   2^16) or a status with pkt_cnt[j] = 0 (GOSSIP_NO_VALUES: every value was
+   this node's).  aux: 2 x the packets' bytes always suffices. */
+int64_t fd_ed25519_gpu_gossip_walk_crds( uint8_t * arena, uint64_t arena_sz, uint64_t aux_off, uint64_t aux_cap,
+                                         fd_ed25519_gpu_span_t const * pkt, uint64_t n, uint8_t const * self,
+                                         fd_ed25519_desc_t * desc, uint64_t desc_cap, int64_t * pkt_desc,
+                                         uint32_t * pkt_cnt );
+/* Walk + one GPU batch: code[k] = the verify code of descriptor k (code_cap
+   entries, pkt_desc / pkt_cnt as above); returns the descriptor count. */
+int64_t fd_ed25519_gpu_gossip_verify_crds( fd_ed25519_gpu_t * ctx, uint8_t * arena, uint64_t arena_sz, uint64_t aux_off,
+                                           uint64_t aux_cap, fd_ed25519_gpu_span_t const * pkt, uint64_t n,
+                                           uint8_t const * self, int8_t * code, uint64_t code_cap, int64_t * pkt_desc,
+                                           uint32_t * pkt_cnt );
 
 /* ---- Shred leader signatures --------------------
 

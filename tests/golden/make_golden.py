@@ -439,6 +439,29 @@ def gen_gossip():
         else:
             p = prune(priv, pub, inner, pr, GOSSIP_SELF, wall)
         pkts.append((60 + t, p))
+    # pull responses / pushes over every CRDS variant, values signed over the
+    # REFERENCE encoder's bytes (so only a walk that re-encodes exactly as
+    # fd_crds_data_encode does verifies them): one per signer, one of this
+    # node's (filtered), one with a flipped signature bit, one unsigned
+    sys.path.insert(0, os.path.dirname(HERE))
+    import crds_gen
+    for disc in range(12):
+        for t in range(2):
+            priv, pub = keys[(disc + t) % 4]
+            sender = pub if disc == 11 else rng.bytes(32)   # contact-info v2: the message's key signs
+            body = None
+            while body is None or gossip_triples(pkt) is None:        # votes: the packet's tail must parse as a txn
+              body = []
+              for i, (d, key) in enumerate([(disc, pub), (disc, GOSSIP_SELF), (disc, pub), ((disc + 5) % 12, None)]):
+                dat = crds_gen.data(rng, d, rng.bytes(32) if key is None else key)
+                one = struct.pack("<I", 2) + sender + struct.pack("<Q", 1) + bytes(64) + dat
+                tr = gossip_triples(one, me=None)
+                sig = sign(tr[0][1], pub, priv) if (i < 3 and tr) else rng.bytes(64)
+                if i == 2:
+                    sig = sig[:5] + bytes([sig[5] ^ 0x20]) + sig[6:]
+                body.append(sig + dat)
+              pkt = struct.pack("<I", 1 + t) + sender + struct.pack("<Q", len(body)) + b"".join(body)
+            pkts.append((200 + 2 * disc + t, pkt))
     pkts.append((90, struct.pack("<I", 7) + rng.bytes(128)))                 # unknown kind
     pkts.append((91, b"\4\0\0"))                                             # short
     out = [GOSSIP_SELF]
