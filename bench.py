@@ -188,6 +188,103 @@ def cpu_baseline(arena, desc, expect, budget_s=10.0):
     return out
 
 
+def shred_cpu_baseline(recs, budget_s):
+    """The reference FEC resolver's per-shred check (oracle/_ref fdref_shred_check:
+    fd_shred_parse, the bmtree root from the inclusion proof, fd_ed25519_verify
+    of the root, src/disco/shred/fd_fec_resolver.c:309-405) on ONE core, as the
+    reference runs it inside its one shred tile: whole passes over the
+    capture's shreds until the budget is spent."""
+    path = os.path.join(REPO, "oracle", "_ref", "libfdref_%s.so" %
+                        ("avx512" if "avx512ifma" in open("/proc/cpuinfo").read() else "ref"))
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.fdref_shred_check.restype = ctypes.c_int
+    lib.fdref_shred_check.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
+    root = ctypes.create_string_buffer(32)
+    for r in recs:                                                           # warm-up pass + check
+        assert lib.fdref_shred_check(r["shred"], len(r["shred"]), r["leader"], root) == 0
+    t0 = time.perf_counter(); done = 0
+    while time.perf_counter() - t0 < budget_s:
+        for r in recs:
+            lib.fdref_shred_check(r["shred"], len(r["shred"]), r["leader"], root)
+        done += len(recs)
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "shreds/s", "cores": 1, "kind": "reference",
+            "sample": "%d passes over the %d valid shreds of the reference's demo capture (%.1f s), "
+                      "fdref_shred_check on one core (the reference checks shreds in one tile)"
+                      % (done // len(recs), len(recs), dt)}
+
+
+def shred_main(args):
+    """--path shred: shreds/s through fd_ed25519_gpu_shred_verify (the
+    FEC resolver's first-shred check as a descriptor source).
+    One step = one call over --batch shreds in HOST memory (the API takes host
+    buffers): host walk (parse, proof bounds), Merkle roots on the GPU
+    (fd_shred_root_kernel), one verify launch, codes back.  Reported beside
+    it: the same with the roots hashed on the host thread
+    (FD_ED25519_GPU_SHRED_HOST_HASH=1), the host walk alone, and the
+    reference's one-core check."""
+    import torch
+    import firedancer_amd as fa
+    from golden_io import read_shreds
+    torch.cuda.set_device(0)
+    base = [r for r in read_shreds() if r["tag"] < 1000 and r["result"] == 0]
+    n = args.batch or 65536
+    blob, spans, keys = bytearray(), [], []
+    key_at = {}
+    for i in range(n):
+        r = base[i % len(base)]
+        if r["leader"] not in key_at:
+            key_at[r["leader"]] = len(blob); blob += r["leader"]
+        keys.append(key_at[r["leader"]])
+        spans.append((len(blob), len(r["shred"]))); blob += r["shred"]
+    aux_off = (len(blob) + 63) & ~63
+    arena = np.zeros(aux_off + 32 * n, np.uint8)
+    arena[:len(blob)] = np.frombuffer(bytes(blob), np.uint8)
+    spans = np.array(spans, fa.SPAN_DTYPE); keys = np.array(keys, np.uint32)
+    g = fa.Ed25519Gpu(device_mask=1, max_batch=n)
+
+    def timed(env_host, steps):
+        if env_host:
+            os.environ["FD_ED25519_GPU_SHRED_HOST_HASH"] = "1"
+        try:
+            for _ in range(args.warmup):
+                out = g.shred_verify(arena, len(arena), aux_off, 32 * n, spans, keys)
+            assert np.all(out == 0), "shred codes differ from the reference's (all valid)"
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                g.shred_verify(arena, len(arena), aux_off, 32 * n, spans, keys)
+            return (time.perf_counter() - t0) / steps
+        finally:
+            os.environ.pop("FD_ED25519_GPU_SHRED_HOST_HASH", None)
+
+    t_gpu = timed(False, args.steps)
+    t_host = timed(True, max(args.steps // 4, 3))
+    host = arena.copy()
+    t0 = time.perf_counter()
+    walks = 3
+    for _ in range(walks):
+        fa.shred_walk(host, len(host), aux_off, 32 * n, spans, keys)
+    t_walk = (time.perf_counter() - t0) / walks
+    line = {"metric": "shreds_verified_per_s", "value": n / t_gpu, "unit": "shreds/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": t_gpu * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "reference demo capture",
+            "config": {"workload": "fd_ed25519_gpu_shred_verify over %d shreds (the %d valid shreds of the "
+                                   "reference's demo-shreds.pcap tiled), host memory in and out" % (n, len(base)),
+                       "batch_per_gpu": n},
+            "host_hash_variant": {"value": n / t_host, "ms_per_step": t_host * 1e3,
+                                  "note": "FD_ED25519_GPU_SHRED_HOST_HASH=1: Merkle roots on the calling thread"},
+            "host_walk_only": {"value": n / t_walk, "ms_per_step": t_walk * 1e3,
+                               "note": "fa.shred_walk: parse + host roots, no GPU (one thread)"},
+            "build": fa.build_id(), "cpu_baseline": None}
+    if not args.no_cpu:
+        line["cpu_baseline"] = shred_cpu_baseline(base, args.cpu_budget)
+    g.close()
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def launch_ranks(args):
     """--gpus N without WORLD_SIZE: run N ranks (one process per GPU) under
     torch.distributed.run as a CHILD process and return its exit code.  The
@@ -240,6 +337,12 @@ def main():
                          "fd_ed25519_gpu_verify_batch_dev launch (the whole batch); -1 (default): 1 when the batch "
                          "is at most one wave per SIMD (256 x CUs signatures: config 2), else 0 (larger batches "
                          "already give every SIMD several waves, and the single-lane kernel packs them better)")
+    ap.add_argument("--path", default="verify", choices=["verify", "shred"],
+                    help="verify (default): the headline line above.  shred: the FEC resolver's first-shred check "
+                         "(fd_ed25519_gpu_shred_verify: host walk, Merkle roots on the GPU, verify) over the "
+                         "reference's demo capture tiled to --batch, from host memory, N=1; a line of its own "
+                         "(not the headline metric) with the host-hash variant and the reference's one-core check "
+                         "(oracle/_ref fdref_shred_check) beside it")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test mode (tests/test_bench_launch.py): gloo, a no-op step on a fixed count; "
                          "exercises the launcher, rank setup and SUM/MAX aggregation without a GPU")
@@ -255,6 +358,11 @@ def main():
         sys.exit(2)
     if args.stub:
         sys.exit(stub_main(args, world, rank))
+    if args.path == "shred":
+        if world != 1:
+            print("bench.py: --path shred runs on one GPU", file=sys.stderr, flush=True)
+            sys.exit(2)
+        sys.exit(shred_main(args))
 
     import torch
     import torch.distributed as dist

@@ -88,7 +88,16 @@ fd_ed25519_gpu_precompile_verify( fd_ed25519_gpu_t * ctx, uint8_t const * arena,
                                   fd_ed25519_gpu_precompile_t const * instr, uint64_t n,
                                   fd_ed25519_gpu_span_t const * txn_instr, uint64_t txn_instr_cnt, int * out ) {
   if( !ctx || (n && (!instr || !out)) ) return FD_ED25519_GPU_ERR_ARG;
-  std::vector<fd_ed25519_desc_t> desc( 255u * n + 1u );
+  /* at most min(count byte, whole 14-byte offset records) descriptors per
+     instruction (not 255 per instruction up front) */
+  uint64_t cap = 1u;
+  for( uint64_t j=0; j<n; j++ ) {
+    uint64_t o = instr[ j ].data.off, dsz = instr[ j ].data.sz;
+    if( dsz < 2u || o + dsz > arena_sz ) continue;      /* the walk reports these */
+    uint64_t c = arena[ o ], rec = (dsz - 2u) / 14u;
+    cap += c < rec ? c : rec;
+  }
+  std::vector<fd_ed25519_desc_t> desc( cap );
   std::vector<uint64_t> first( n + 1u );      /* descriptors of instruction j: [first[j], first[j+1]) */
   std::vector<int>      tail( n + 1u );       /* the error after its last descriptor, or 0 */
   int64_t nd = fd_ed25519_gpu_precompile_walk( arena, arena_sz, instr, n, txn_instr, txn_instr_cnt,
