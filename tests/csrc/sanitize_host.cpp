@@ -273,7 +273,7 @@ static void check_precompile( int iters ) {
 /* Gossip packets: well-formed ping / pong / prune layouts (random counts,
    lengths off by a few bytes) and random bytes, in exact-size arenas with
    the aux region after them. */
-static uint64_t st_gossip = 0;
+static uint64_t st_gossip = 0, st_crds = 0;
 static void check_gossip( int iters ) {
   for( int it=0; it<iters; it++ ) {
     std::vector<uint8_t> a; std::vector<fd_ed25519_gpu_span_t> pk;
@@ -287,8 +287,21 @@ static void check_gossip( int iters ) {
         sz = 4 + 32 + 32 + 8 + 32 * (n & 15) + 64 + 32 + 8 + (rnd( 3 ) ? 0 : rnd( 5 ) - 2);
         for( uint64_t i=0; i<sz; i++ ) a.push_back( (uint8_t)rng() );
         if( sz >= 76 ) memcpy( &a[ off + 68 ], &n, 8 );
+      } else if( (kind == 1 || kind == 2) && rnd( 2 ) ) {           /* CRDS: sender, count, values */
+        uint64_t n = rnd( 5 );
+        sz = 4 + 32 + 8;
+        for( uint64_t i=0; i<sz; i++ ) a.push_back( (uint8_t)rng() );
+        memcpy( &a[ off + 36 ], &n, 8 );
+        for( uint64_t v=0; v<n; v++ ) {
+          uint32_t disc = rnd( 2 ) ? 8u : (uint32_t)rnd( 13 );          /* 8: node_instance, 56 bytes */
+          uint64_t vsz = 64 + 4 + ((disc == 8 && rnd( 4 )) ? 56 : rnd( 160 ));
+          for( uint64_t i=0; i<vsz; i++ ) a.push_back( (uint8_t)(rnd( 3 ) ? rnd( 3 ) : rng()) );
+          memcpy( &a[ off + sz + 64 ], &disc, 4 );
+          sz += vsz;
+        }
+        if( !rnd( 3 ) ) { uint64_t cut = rnd( 8 ); while( cut-- && sz > 4 ) { a.pop_back(); sz--; } }
       } else sz = rnd( 300 );
-      if( kind != 3 ) for( uint64_t i=0; i<sz; i++ ) a.push_back( (uint8_t)rng() );
+      if( kind != 3 && a.size() == off ) for( uint64_t i=0; i<sz; i++ ) a.push_back( (uint8_t)rng() );
       if( sz >= 4 ) memcpy( &a[ off ], &kind, 4 );
       pk.push_back( { (uint32_t)off, (uint32_t)sz } );
     }
@@ -307,6 +320,17 @@ static void check_gossip( int iters ) {
     fd_ed25519_gpu_t ctx; ctx.pend = 0;
     if( fd_ed25519_gpu_gossip_verify( &ctx, ar.p, ar.n, aux_off, aux_cap, pk.data(), np, me, out.data() ) ) {
       fprintf( stderr, "gossip_verify\n" ); exit( 1 );
+    }
+    /* the CRDS walk: every value decoded and re-encoded into aux (too small
+       for them at times: ERR_ARG, never a write past it) */
+    std::vector<fd_ed25519_desc_t> cdesc( np + ar.n / 64 + 1 ); std::vector<uint32_t> pc( np );
+    int64_t nc = fd_ed25519_gpu_gossip_walk_crds( ar.p, ar.n, aux_off, aux_cap, pk.data(), np, rnd( 2 ) ? me : NULL,
+                                                  cdesc.data(), cdesc.size(), pd.data(), pc.data() );
+    if( nc < 0 && nc != FD_ED25519_GPU_ERR_ARG ) { fprintf( stderr, "gossip crds walk %ld\n", (long)nc ); exit( 1 ); }
+    if( nc > 0 ) {
+      st_crds += (uint64_t)nc;
+      std::vector<int8_t> cc( (size_t)nc );
+      if( stand_in_verify( ar.p, ar.n, cdesc.data(), (uint64_t)nc, cc.data() ) ) { fprintf( stderr, "crds desc outside\n" ); exit( 1 ); }
     }
     if( fd_ed25519_gpu_gossip_walk( ar.p, ar.n, 0, 4, pk.data(), np, NULL, desc.data(), np, pd.data() ) != FD_ED25519_GPU_ERR_ARG &&
         pk[ 0 ].sz ) { fprintf( stderr, "aux over a packet accepted\n" ); exit( 1 ); }
@@ -415,9 +439,10 @@ int main( int argc, char ** argv ) {
   check_shreds( 1500 * scale );
   check_offload( 20000 * scale );
   printf( "sanitize_host: ok (frags: %lu parsed ok, %lu failed, %lu bad, %lu descriptors; precompile %lu descriptors; "
-          "gossip %lu descriptors; shreds %lu descriptors; link %lu published, %lu taken, %lu joins refused)\n",
+          "gossip %lu descriptors; crds %lu descriptors; shreds %lu descriptors; link %lu published, %lu taken, "
+          "%lu joins refused)\n",
           (unsigned long)st_ok, (unsigned long)st_failed, (unsigned long)st_bad, (unsigned long)st_desc, (unsigned long)st_walk,
-          (unsigned long)st_gossip, (unsigned long)st_shred, (unsigned long)st_pub,
+          (unsigned long)st_gossip, (unsigned long)st_crds, (unsigned long)st_shred, (unsigned long)st_pub,
           (unsigned long)st_avail, (unsigned long)st_join_refused );
   return 0;
 }

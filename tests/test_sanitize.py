@@ -1,7 +1,7 @@
 """CPU: AddressSanitizer + UndefinedBehaviorSanitizer over the host code that
 parses attacker-shaped bytes: the frag ->
 descriptor parse, the tcache, the sync and async verify stages (host parse),
-the precompile record walk, the gossip packet walk, the shred walk and the
+the precompile record walk, the gossip packet walks (CRDS values included), the shred walk and the
 offload shared-memory link.
 
 1. tests/csrc/sanitize_host.cpp: those product sources compiled with
@@ -36,7 +36,7 @@ def test_sanitized_driver():
     import re
     nums = [int(x) for x in re.findall(r"(\d+) (?:parsed ok|failed|bad|descriptors|published|taken|joins refused)",
                                         r.stdout)]
-    assert len(nums) == 10 and min(nums) > 0, r.stdout
+    assert len(nums) == 11 and min(nums) > 0, r.stdout
 
 
 def test_cpu_suites_against_asan_libraries():
