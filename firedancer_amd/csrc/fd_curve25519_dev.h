@@ -54,7 +54,15 @@ FD_FN void ge_identity( ge_p3 & p ) { fe_set0( p.X ); fe_set1( p.Y ); fe_set1( p
    Here and in ge_madd, F and H are the FIRST operands and E, G the second:
    F is then left uncarried (bound class "F" of fd_f25519_dev.h: its x19 would
    not fit 32 bits, its x2 does, and F x M column sums stay below 2^63),
-   which drops one fe_carry per doubling / mixed addition. */
+   which drops one fe_carry per doubling / mixed addition.
+   The formula wants G = YY-XX and E = (X+Y)^2-XX-YY; here both come out
+   NEGATED at no subtraction of their own: G' = XX-YY (+2p) = -G, and
+   E' = H + (-(X+Y)^2) with the square produced in complement form
+   (fe_sq_neg: the negation is in the product's finish), so E' = -E is one
+   limb-pair addition.  F = 2ZZ-G = 2ZZ+G' needs no 4p-G either.  Every
+   output product then carries exactly one negated factor except Z
+   (F*G' = -FG... see below): X' = F E' = -X, Y' = H G' = -Y, Z' = F G' = -Z,
+   T' = H E' = -T, i.e. (-X,-Y,-Z,-T), the same projective point as 2p. */
 FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
   fe XX, YY, ZZ, s, H, G, E, Fn;
   fe_sq( XX, p.X );                     /* R */
@@ -64,20 +72,19 @@ FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
   fe_sq( ZZ, p.Z );                     /* R */
   FE_FENCE();
   fe_add( H, YY, XX );                  /* M   H = YY+XX, not carried: first operand only */
-  fe_sub4p( G, H );                     /*     4p - H, the addend that subtracts H        */
   fe_add( s, p.X, p.Y );                /* M */
-  fe_sq_seed( E, s, G );                /* R   E = (X+Y)^2-YY-XX = 2XY, carried by the square */
+  fe_sq_neg( E, s );                    /* N   -(X+Y)^2, complement form (limb 1 < 2^26) */
   FE_FENCE();
-  fe_sub( G, YY, XX );                  /* M   G = YY-XX+2p       */
-  fe_sub4p( s, G );                     /*     4p-G = XX-YY+2p limbwise (G < 4p per limb) */
-  fe_lshl1_add( Fn, ZZ, s );            /* F   Fn = 2ZZ-G, not carried: first operand only */
-  fe_mul( r.X, Fn, E );
+  fe_add( E, E, H );                    /* E'  = XX+YY-(X+Y)^2 = -2XY: a second operand only */
+  fe_sub( G, XX, YY );                  /* M   G' = XX-YY+2p = -G */
+  fe_lshl1_add( Fn, ZZ, G );            /* F   Fn = 2ZZ+G' = 2ZZ-G, not carried: first operand only */
+  fe_mul( r.X, Fn, E );                 /* -X */
   FE_FENCE();
-  fe_mul( r.Y, H, G );
+  fe_mul( r.Y, H, G );                  /* -Y */
   FE_FENCE();
-  fe_mul( r.Z, Fn, G );
+  fe_mul( r.Z, Fn, G );                 /* -Z */
   FE_FENCE();
-  if( want_t ) fe_mul( r.T, H, E );
+  if( want_t ) fe_mul( r.T, H, E );     /* -T */
   FE_FENCE();
 }
 

@@ -251,15 +251,14 @@ __device__ __forceinline__ void vtab_fetch( uint32_t w[ 40 ], uint32_t const * v
 
 __device__ __forceinline__ void vtab_finish( ge_cached & c, uint32_t const w[ 40 ], uint32_t db ) {
   bool neg = db < 8u;
-  fe tv, tn;
+  fe tv;
 #pragma unroll
   for( int j=0; j<10; j++ ) { tv.v[j] = w[FD_VW(2,j)]; c.Z2.v[j] = w[FD_VW(3,j)]; }
-  fe_neg( tn, tv );
+  fe_cneg( c.T2d, tv, neg );
 #pragma unroll
   for( int j=0; j<10; j++ ) {
     c.YpX.v[j] = neg ? w[FD_VW(1,j)] : w[FD_VW(0,j)];
     c.YmX.v[j] = neg ? w[FD_VW(0,j)] : w[FD_VW(1,j)];
-    c.T2d.v[j] = neg ? tn.v[j] : tv.v[j];
   }
 }
 
@@ -274,15 +273,14 @@ __device__ __forceinline__ void ctab_fetch( uint32_t w[ 32 ], uint32_t const * c
 
 __device__ __forceinline__ void ctab_finish( ge_precomp & q, uint32_t const w[ 32 ], int d ) {
   bool neg = d < 0;
-  fe t, tn;
+  fe t;
 #pragma unroll
   for( int j=0; j<10; j++ ) t.v[j] = w[20+j];
-  fe_neg( tn, t );
+  fe_cneg( q.T2d, t, neg );
 #pragma unroll
   for( int j=0; j<10; j++ ) {
     q.YpX.v[j] = neg ? w[10+j] : w[j];
     q.YmX.v[j] = neg ? w[j]    : w[10+j];
-    q.T2d.v[j] = neg ? tn.v[j] : t.v[j];
   }
 }
 
@@ -594,12 +592,10 @@ __device__ __forceinline__ void lds_entry_words( uint32_t w[ 4*NC ], uint4 const
 /* The cached entry from lds_entry_words' words: 2dT negated for a negative
    digit (Y+X / Y-X came swapped). */
 __device__ __forceinline__ void lds_entry_finish( ge_cached & c, uint32_t const w[ 40 ], bool neg ) {
-  fe tv, tn;
+  fe tv;
 #pragma unroll
   for( int j=0; j<10; j++ ) { c.YpX.v[j] = w[j]; c.YmX.v[j] = w[10+j]; tv.v[j] = w[20+j]; c.Z2.v[j] = w[30+j]; }
-  fe_neg( tn, tv );
-#pragma unroll
-  for( int j=0; j<10; j++ ) c.T2d.v[j] = neg ? tn.v[j] : tv.v[j];
+  fe_cneg( c.T2d, tv, neg );
 }
 
 /* Biased 4-bit digit i (0..16) of a recoded scalar y = x + 8 (16^0 + ... +

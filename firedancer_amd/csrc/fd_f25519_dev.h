@@ -45,6 +45,8 @@ struct fe { uint32_t v[ 10 ]; };
 
 #define FE_M26 0x3ffffffu
 #define FE_M25 0x1ffffffu
+/* column-0 addend of a complement-form product (fe_sq_neg): 18 + 2^51 */
+#define FE_NEG_SEED ( 18ull + (1ull << 51) )
 
 /* 2p and 4p in limb form (limb 0 of p is 2^26-19, others 2^26-1 / 2^25-1) */
 #define FE_2P0  (2u*(0x3ffffffu-18u))
@@ -73,16 +75,52 @@ FD_FN uint64_t col5( uint64_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t
 FD_FN void fe_set0( fe & r ) { for( int i=0; i<10; i++ ) r.v[i] = 0u; }
 FD_FN void fe_set1( fe & r ) { r.v[0] = 1u; for( int i=1; i<10; i++ ) r.v[i] = 0u; }
 
+/* Limb pairs.  Every limb stays below 2^31, so a 64-bit add (or a 64-bit
+   shift left by one) of two limb pairs never carries out of the low limb:
+   it is exactly two independent 32-bit operations, in ONE issue slot
+   (v_lshl_add_u64 / v_lshlrev_b64 take the same slot as a v_add_u32 when
+   several waves share the SIMD, profiles/r03/probes).  As asm: the compiler
+   would otherwise split the 64-bit add back into two 32-bit ones (it may
+   assume a carry between the halves). */
+FD_FN uint64_t fe_pk( uint32_t lo, uint32_t hi ) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+#if defined(__HIP_DEVICE_COMPILE__)
+FD_FN uint64_t pk_add( uint64_t a, uint64_t b ) {
+  uint64_t r; asm( "v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b) ); return r;
+}
+FD_FN uint64_t pk_add_s( uint64_t a, uint64_t s ) {      /* s: a wave-uniform pair (SGPRs) */
+  uint64_t r; asm( "v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "s"(s) ); return r;
+}
+FD_FN uint64_t pk_shl1_add( uint64_t a, uint64_t b ) {
+  uint64_t r; asm( "v_lshl_add_u64 %0, %1, 1, %2" : "=v"(r) : "v"(a), "v"(b) ); return r;
+}
+FD_FN uint64_t pk_shl1( uint64_t a ) {
+  uint64_t r; asm( "v_lshlrev_b64 %0, 1, %1" : "=v"(r) : "v"(a) ); return r;
+}
+#else
+FD_FN uint64_t pk_add( uint64_t a, uint64_t b ) { return a + b; }
+FD_FN uint64_t pk_add_s( uint64_t a, uint64_t s ) { return a + s; }
+FD_FN uint64_t pk_shl1_add( uint64_t a, uint64_t b ) { return (a << 1) + b; }
+FD_FN uint64_t pk_shl1( uint64_t a ) { return a << 1; }
+#endif
+#define FE_PK( f, i ) fe_pk( (f).v[2*(i)], (f).v[2*(i)+1] )
+#define FE_UNPK( r, i, x ) do { uint64_t _x = (x); (r).v[2*(i)] = (uint32_t)_x; (r).v[2*(i)+1] = (uint32_t)(_x >> 32); } while( 0 )
+
 FD_FN void fe_add( fe & r, fe const & a, fe const & b ) {
 #pragma unroll
-  for( int i=0; i<10; i++ ) r.v[i] = a.v[i] + b.v[i];
+  for( int i=0; i<5; i++ ) FE_UNPK( r, i, pk_add( FE_PK( a, i ), FE_PK( b, i ) ) );
 }
 
-/* r = a + 2p - b.  Requires b limbs <= 2p limbs (b in R). */
+/* r = a + 2p - b.  Requires b limbs <= 2p limbs (b in R).  a + 2p as limb
+   pairs first (no limb goes negative), then the ten subtractions. */
+#define FE_2P_PK0 ( (uint64_t)FE_2P0 | ((uint64_t)FE_2PO << 32) )
+#define FE_2P_PK  ( (uint64_t)FE_2PE | ((uint64_t)FE_2PO << 32) )
 FD_FN void fe_sub( fe & r, fe const & a, fe const & b ) {
-  r.v[0] = (a.v[0] + FE_2P0) - b.v[0];
+  fe t;
+  FE_UNPK( t, 0, pk_add_s( FE_PK( a, 0 ), FE_2P_PK0 ) );
 #pragma unroll
-  for( int i=1; i<10; i++ ) r.v[i] = (a.v[i] + ((i&1) ? FE_2PO : FE_2PE)) - b.v[i];
+  for( int i=1; i<5; i++ ) FE_UNPK( t, i, pk_add_s( FE_PK( a, i ), FE_2P_PK ) );
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = t.v[i] - b.v[i];
 }
 
 /* One parallel carry round: limbs < 2^31 in, R out. */
@@ -113,13 +151,7 @@ FD_FN void fe_sub4p( fe & r, fe const & a ) {
    the compiler would otherwise reassociate the sum into two adds). */
 FD_FN void fe_lshl1_add( fe & r, fe const & a, fe const & b ) {
 #pragma unroll
-  for( int i=0; i<10; i++ ) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm( "v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r.v[i]) : "v"(a.v[i]), "v"(b.v[i]) );
-#else
-    r.v[i] = (a.v[i] << 1) + b.v[i];
-#endif
-  }
+  for( int i=0; i<5; i++ ) FE_UNPK( r, i, pk_shl1_add( FE_PK( a, i ), FE_PK( b, i ) ) );
 }
 
 /* 2p - a (a in R) -> M */
@@ -127,6 +159,23 @@ FD_FN void fe_neg( fe & r, fe const & a ) {
   r.v[0] = FE_2P0 - a.v[0];
 #pragma unroll
   for( int i=1; i<10; i++ ) r.v[i] = ((i&1) ? FE_2PO : FE_2PE) - a.v[i];
+}
+
+/* r = neg ? 2p - a : a (a in R) per lane: (a ^ m) + (m & (2p+1)) with
+   m = neg ? ~0 : 0 is -a-1+2p+1 or a, one v_xad_u32 per limb (plus the
+   mask and its three limb constants) instead of a negation and a select. */
+FD_FN void fe_cneg( fe & r, fe const & a, bool neg ) {
+  uint32_t m = neg ? ~0u : 0u;
+  uint32_t c0 = m & (FE_2P0 + 1u), ce = m & (FE_2PE + 1u), co = m & (FE_2PO + 1u);
+#pragma unroll
+  for( int i=0; i<10; i++ ) {
+    uint32_t c = i == 0 ? c0 : ((i & 1) ? co : ce);
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm( "v_xad_u32 %0, %1, %2, %3" : "=v"(r.v[i]) : "v"(a.v[i]), "v"(m), "v"(c) );
+#else
+    r.v[i] = (a.v[i] ^ m) + c;
+#endif
+  }
 }
 
 /* Column finish: split the 64-bit column into its limb and carry the rest
@@ -240,6 +289,32 @@ FD_FN void fe_sq_seed( fe & h, fe const & f, fe const & s ) {
   h0 = (uint32_t)a & FE_M26;
   h1 += (uint32_t)(a >> 26);
   h.v[0]=h0; h.v[1]=h1; h.v[2]=h2; h.v[3]=h3; h.v[4]=h4; h.v[5]=h5; h.v[6]=h6; h.v[7]=h7; h.v[8]=h8; h.v[9]=h9;
+}
+
+/* h = -f^2 in fe_finish_neg's complement form (fd_f25519_asm.h): the square
+   of f plus FE_NEG_SEED, carried, then every limb taken from its mask
+   (limb 1 from 2^26 - 1).  Input in M; output limbs like R except limb 1
+   (up to 2^26). */
+FD_FN void fe_sq_neg( fe & h, fe const & f ) {
+  uint32_t f0=f.v[0],f1=f.v[1],f2=f.v[2],f3=f.v[3],f4=f.v[4],f5=f.v[5],f6=f.v[6],f7=f.v[7],f8=f.v[8],f9=f.v[9];
+  uint32_t f0_2=2u*f0, f1_2=2u*f1, f2_2=2u*f2, f3_2=2u*f3, f4_2=2u*f4, f5_2=2u*f5, f6_2=2u*f6, f7_2=2u*f7;
+  uint32_t f5_38=38u*f5, f6_19=19u*f6, f7_38=38u*f7, f8_19=19u*f8, f9_38=38u*f9;
+  uint64_t c[ 10 ];
+  c[0] = col5( (uint64_t)f0*f0 + FE_NEG_SEED, f1_2,f9_38, f2_2,f8_19, f3_2,f7_38, f4_2,f6_19, f5,f5_38 );
+  c[1] = col5( c[0] >> 26, f0_2,f1, f2,f9_38, f3_2,f8_19, f4,f7_38, f5_2,f6_19 );
+  c[2] = mad64( f0_2,f2, col5( c[1] >> 25, f1_2,f1, f3_2,f9_38, f4_2,f8_19, f5_2,f7_38, f6,f6_19 ) );
+  c[3] = col5( c[2] >> 26, f0_2,f3, f1_2,f2, f4,f9_38, f5_2,f8_19, f6,f7_38 );
+  c[4] = mad64( f0_2,f4, col5( c[3] >> 25, f1_2,f3_2, f2,f2, f5_2,f9_38, f6_2,f8_19, f7,f7_38 ) );
+  c[5] = col5( c[4] >> 26, f0_2,f5, f1_2,f4, f2_2,f3, f6,f9_38, f7_2,f8_19 );
+  c[6] = mad64( f0_2,f6, col5( c[5] >> 25, f1_2,f5_2, f2_2,f4, f3_2,f3, f7_2,f9_38, f8,f8_19 ) );
+  c[7] = col5( c[6] >> 26, f0_2,f7, f1_2,f6, f2_2,f5, f3_2,f4, f8,f9_38 );
+  c[8] = mad64( f0_2,f8, col5( c[7] >> 25, f1_2,f7_2, f2_2,f6, f3_2,f5_2, f4,f4, f9,f9_38 ) );
+  c[9] = col5( c[8] >> 26, f0_2,f9, f1_2,f8, f2_2,f7, f3_2,f6, f4_2,f5 );
+  uint64_t t = c[9] >> 25;
+  uint64_t a = 19u*t + ((uint32_t)c[0] & FE_M26);
+  for( int i=0; i<10; i++ ) h.v[i] = ~(uint32_t)c[i] & ((i&1) ? FE_M25 : FE_M26);
+  h.v[0] = ~(uint32_t)a & FE_M26;
+  h.v[1] += (1u << 25) - (uint32_t)(a >> 26);
 }
 
 FD_FN void fe_mul2( fe & h, fe const & f, fe const & g, fe & k, fe const & p, fe const & q ) { fe_mul( h, f, g ); fe_mul( k, p, q ); }

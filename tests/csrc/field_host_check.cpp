@@ -11,6 +11,10 @@ void t_sub( uint32_t * h, uint32_t const * f, uint32_t const * g ) { fe a, b, r;
 void t_carry( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_carry( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
 void t_tobytes( uint32_t * o, uint32_t const * f ) { fe a; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_tobytes32( o, a ); }
 void t_frombytes( uint32_t * h, uint32_t const * w ) { fe a; fe_frombytes32( a, w ); for( int i=0;i<10;i++ ) h[i]=a.v[i]; }
+void t_sq_neg( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_sq_neg( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_add( uint32_t * h, uint32_t const * f, uint32_t const * g ) { fe a, b, r; for( int i=0;i<10;i++ ){a.v[i]=f[i];b.v[i]=g[i];} fe_add( r, a, b ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_lshl1_add( uint32_t * h, uint32_t const * f, uint32_t const * g ) { fe a, b, r; for( int i=0;i<10;i++ ){a.v[i]=f[i];b.v[i]=g[i];} fe_lshl1_add( r, a, b ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
+void t_cneg( uint32_t * h, uint32_t const * f, int neg ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_cneg( r, a, neg != 0 ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
 void t_pow22523( uint32_t * h, uint32_t const * f ) { fe a, r; for( int i=0;i<10;i++ ) a.v[i]=f[i]; fe_pow22523( r, a ); for( int i=0;i<10;i++ ) h[i]=r.v[i]; }
 }
 #include "../../firedancer_amd/csrc/fd_scalar_dev.h"
@@ -36,4 +40,13 @@ void t_comb_digits( int * d, uint32_t const * w ) {
 #include "../../firedancer_amd/csrc/fd_lattice_dev.h"
 extern "C" {
 int t_lattice( uint32_t const * k, uint32_t * u, uint32_t * v, int * u_neg ) { return lat_short_vector( k, u, v, u_neg ); }
+}
+#include "../../firedancer_amd/csrc/fd_curve25519_dev.h"
+extern "C" {
+/* p: X,Y,Z,T (40 limbs) -> r = 2p with T (40 limbs) */
+void t_dbl( uint32_t * r, uint32_t const * p ) {
+  ge_p3 a, o; for( int i=0;i<10;i++ ){ a.X.v[i]=p[i]; a.Y.v[i]=p[10+i]; a.Z.v[i]=p[20+i]; a.T.v[i]=p[30+i]; }
+  ge_dbl( o, a, true );
+  for( int i=0;i<10;i++ ){ r[i]=o.X.v[i]; r[10+i]=o.Y.v[i]; r[20+i]=o.Z.v[i]; r[30+i]=o.T.v[i]; }
+}
 }

@@ -223,3 +223,106 @@ def test_comb_digits(lib):
         assert 0x7fffffff not in dd, w
         assert sum(x << (23 * k) for k, x in enumerate(dd)) == w, w
         assert all(-2**22 <= x < 2**22 for x in dd[:10]) and 0 <= dd[10] <= 2**22, (w, dd)
+
+
+N_1 = 2**26 - 1    # fe_sq_neg / fe_finish_neg: limb 1 taken from 2^26 - 1
+
+
+def in_N(h):
+    return all(0 <= x <= ((2**26 - 1) if i % 2 == 0 else (2**25 - 1)) for i, x in enumerate(h) if i != 1) and 0 <= h[1] <= N_1
+
+
+def test_sq_neg_complement(lib):
+    """fe_sq_neg: -f^2 in complement form (column 0 seeded with 18 + 2^51, every
+    limb taken from its mask, limb 1 from 2^26 - 1): exact mod p at the M bounds,
+    limbs never negative."""
+    rng = random.Random(21)
+    for it in range(4000):
+        mode = "max" if it < 20 else "rand"
+        f = limbs_at(M_E, M_O, mode, rng)
+        if it % 7 == 3:
+            f = [0] * 10; f[rng.randrange(10)] = rng.randrange(0, 3)     # tiny values: the seed carries through
+        h = (ctypes.c_uint32 * 10)(); lib.t_sq_neg(h, arr(f)); h = list(h)
+        assert val(h) % P == (-val(f) ** 2) % P and in_N(h), (f, h)
+
+
+def test_dbl_operands_at_bounds(lib):
+    """ge_dbl's negated operands: E' = (XX + YY) + (-(X+Y)^2) (2R + N, a second
+    operand) and G' = XX + 2p - YY; X' = Fn E' and T' = H E' stay exact and in R
+    with Fn at the F bound and E' at its own largest limbs."""
+    rng = random.Random(23)
+    r = [R_E if i % 2 == 0 else R_O for i in range(10)]
+    n = [(2**26 - 1) if i % 2 == 0 else (2**25 - 1) for i in range(10)]; n[1] = N_1
+    ep_max = [2 * r[i] + n[i] for i in range(10)]
+    assert all(19 * x < 2**32 for x in ep_max)
+    for it in range(3000):
+        mode = "max" if it < 20 else "rand"
+        ep = [x if mode == "max" else rng.randrange(0, x + 1) for x in ep_max]
+        f = limbs_at(F_E, F_O, mode, rng); hh = [2 * x if mode == "max" else rng.randrange(0, 2 * x + 1) for x in r]
+        h = (ctypes.c_uint32 * 10)(); lib.t_mul(h, arr(f), arr(ep)); h = list(h)
+        assert val(h) % P == val(f) * val(ep) % P and in_R(h)
+        h = (ctypes.c_uint32 * 10)(); lib.t_mul(h, arr(hh), arr(ep)); h = list(h)
+        assert val(h) % P == val(hh) * val(ep) % P and in_R(h)
+
+
+def test_pair_ops_and_cneg(lib):
+    """fe_add / fe_lshl1_add / fe_sub as limb-pair (64-bit) operations equal the
+    limbwise ones at the F bound (no carry between the halves); fe_cneg is
+    2p - a or a."""
+    rng = random.Random(29)
+    two_p = [2 * (2**26 - 19)] + [2 * (2**26 - 1) if i % 2 == 0 else 2 * (2**25 - 1) for i in range(1, 10)]
+    for it in range(2000):
+        mode = "max" if it < 10 else "rand"
+        a = limbs_at(F_E, F_O, mode, rng); b = limbs_at(M_E, M_O, mode, rng)
+        h = (ctypes.c_uint32 * 10)(); lib.t_add(h, arr(a), arr(b)); assert list(h) == [a[i] + b[i] for i in range(10)]
+        z = limbs_at(R_E, R_O, mode, rng)
+        h = (ctypes.c_uint32 * 10)(); lib.t_lshl1_add(h, arr(z), arr(b)); assert list(h) == [2 * z[i] + b[i] for i in range(10)]
+        x = limbs_at(R_E, R_O, mode, rng); y = limbs_at(R_E, R_O, mode, rng)
+        h = (ctypes.c_uint32 * 10)(); lib.t_sub(h, arr(x), arr(y)); assert list(h) == [x[i] + two_p[i] - y[i] for i in range(10)]
+        for neg in (0, 1):
+            h = (ctypes.c_uint32 * 10)(); lib.t_cneg(h, arr(x), neg)
+            assert list(h) == ([two_p[i] - x[i] for i in range(10)] if neg else x)
+
+
+D_ED = (-121665 * pow(121666, P - 2, P)) % P
+
+
+def _ed_add(p1, p2):
+    x1, y1 = p1; x2, y2 = p2
+    t = D_ED * x1 * x2 * y1 * y2 % P
+    return ((x1 * y2 + y1 * x2) * pow(1 + t, P - 2, P) % P, (y1 * y2 + x1 * x2) * pow(1 - t, P - 2, P) % P)
+
+
+def _limbs(x):
+    out = []
+    for i in range(10):
+        w = (26 if i % 2 == 0 else 25)
+        out.append(x >> POS[i] & ((1 << w) - 1))
+    return out
+
+
+def test_dbl_host_projective(lib):
+    """ge_dbl (negated E' and G', every output coordinate negated: the same
+    projective point) against affine big-int doubling from random multiples of
+    the base point, projectively scaled by a random Z."""
+    rng = random.Random(31)
+    by = 4 * pow(5, P - 2, P) % P
+    bx2 = (by * by - 1) * pow(D_ED * by * by + 1, P - 2, P) % P
+    bx = pow(bx2, (P + 3) // 8, P)
+    if (bx * bx - bx2) % P:
+        bx = bx * pow(2, (P - 1) // 4, P) % P
+    if bx & 1:
+        bx = P - bx
+    pt = (bx, by)
+    for it in range(60):
+        pt = _ed_add(pt, (bx, by)) if it % 3 else _ed_add(pt, pt)
+        z = rng.randrange(1, P)
+        X, Y, Z, T = pt[0] * z % P, pt[1] * z % P, z, pt[0] * pt[1] * z % P
+        inp = _limbs(X) + _limbs(Y) + _limbs(Z) + _limbs(T)
+        o = (ctypes.c_uint32 * 40)(); lib.t_dbl(o, arr(inp)); o = list(o)
+        X3, Y3, Z3, T3 = (val(o[10 * k:10 * k + 10]) % P for k in range(4))
+        ex = _ed_add(pt, pt)
+        zi = pow(Z3, P - 2, P)
+        assert (X3 * zi % P, Y3 * zi % P) == ex
+        assert T3 * Z3 % P == X3 * Y3 % P
+        assert all(in_R(o[10 * k:10 * k + 10]) for k in range(4))

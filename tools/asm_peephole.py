@@ -12,7 +12,8 @@ and the assembler (firedancer_amd/Makefile):
   2. The s_nop 0 the compiler places after each inline-asm block (it cannot
      see inside asm and pads conservatively) is dropped when the block holds
      only v_mad_u64_u32 / v_lshrrev_b64 (the field-product chains of
-     fd_f25519_dev.h) and the next instruction is a plain ALU op from the
+     fd_f25519_dev.h) or the limb-pair / mask / negation helpers
+     (v_lshl_add_u64, v_lshlrev_b64, v_bfi_b32, v_xad_u32) and the next instruction is a plain ALU op from the
      whitelist below -- the same pairs the compiler itself emits back to back
      with no wait state when it generates those instructions.
 
@@ -36,9 +37,10 @@ SAFE_AFTER_ASM = {
     "v_and_b32_e32", "v_and_b32_e64", "v_lshrrev_b64", "v_lshlrev_b64", "v_add_u32_e32", "v_add_u32_e64",
     "v_sub_u32_e32", "v_sub_u32_e64", "v_mad_u64_u32", "v_mov_b32_e32", "v_mov_b64_e32", "v_lshl_add_u64",
     "v_mul_lo_u32", "v_lshlrev_b32_e32", "v_lshrrev_b32_e32", "v_add3_u32", "v_alignbit_b32",
-    "v_mul_u32_u24_e32", "v_mad_u32_u24", "v_or_b32_e32", "v_xor_b32_e32", "v_bfi_b32",
+    "v_mul_u32_u24_e32", "v_mad_u32_u24", "v_or_b32_e32", "v_xor_b32_e32", "v_bfi_b32", "v_xad_u32",
+    "v_lshl_add_u32", "v_cndmask_b32_e64",
 }
-ASM_BODY_OK = {"v_mad_u64_u32", "v_lshrrev_b64"}
+ASM_BODY_OK = {"v_mad_u64_u32", "v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64", "v_bfi_b32", "v_xad_u32"}
 
 
 def is_inline_or_reg(op):
