@@ -38,7 +38,7 @@ SAFE_AFTER_ASM = {
     "v_sub_u32_e32", "v_sub_u32_e64", "v_mad_u64_u32", "v_mov_b32_e32", "v_mov_b64_e32", "v_lshl_add_u64",
     "v_mul_lo_u32", "v_lshlrev_b32_e32", "v_lshrrev_b32_e32", "v_add3_u32", "v_alignbit_b32",
     "v_mul_u32_u24_e32", "v_mad_u32_u24", "v_or_b32_e32", "v_xor_b32_e32", "v_bfi_b32", "v_xad_u32",
-    "v_lshl_add_u32", "v_cndmask_b32_e64",
+    "v_lshl_add_u32", "v_cndmask_b32_e64", "v_bitop3_b32", "v_perm_b32",
 }
 ASM_BODY_OK = {"v_mad_u64_u32", "v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64", "v_bfi_b32", "v_xad_u32"}
 
