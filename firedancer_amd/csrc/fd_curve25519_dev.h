@@ -60,9 +60,9 @@ FD_FN void ge_identity( ge_p3 & p ) { fe_set0( p.X ); fe_set1( p.Y ); fe_set1( p
    E' = H + (-(X+Y)^2) with the square produced in complement form
    (fe_sq_neg: the negation is in the product's finish), so E' = -E is one
    limb-pair addition.  F = 2ZZ-G = 2ZZ+G' needs no 4p-G either.  Every
-   output product then carries exactly one negated factor except Z
-   (F*G' = -FG... see below): X' = F E' = -X, Y' = H G' = -Y, Z' = F G' = -Z,
-   T' = H E' = -T, i.e. (-X,-Y,-Z,-T), the same projective point as 2p. */
+   output product then carries exactly one negated factor: X' = F E' = -X,
+   Y' = H G' = -Y, Z' = F G' = -Z, T' = H E' = -T, i.e. (-X,-Y,-Z,-T), the
+   same projective point as 2p. */
 FD_GE_FN void ge_dbl( ge_p3 & r, ge_p3 const & p, bool want_t ) {
   fe XX, YY, ZZ, s, H, G, E, Fn;
   fe_sq( XX, p.X );                     /* R */

@@ -147,8 +147,8 @@ FD_FN void fe_sub4p( fe & r, fe const & a ) {
   for( int i=1; i<10; i++ ) r.v[i] = ((i&1) ? FE_4PO : FE_4PE) - a.v[i];
 }
 
-/* r = 2a + b limbwise, one v_lshl_add_u32 per limb on the device (as asm:
-   the compiler would otherwise reassociate the sum into two adds). */
+/* r = 2a + b limbwise: one v_lshl_add_u64 per limb pair on the device
+   (a's limbs below 2^31, so no bit crosses into the high limb). */
 FD_FN void fe_lshl1_add( fe & r, fe const & a, fe const & b ) {
 #pragma unroll
   for( int i=0; i<5; i++ ) FE_UNPK( r, i, pk_shl1_add( FE_PK( a, i ), FE_PK( b, i ) ) );
