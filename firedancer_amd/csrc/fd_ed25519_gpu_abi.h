@@ -184,6 +184,7 @@ struct shred_root_args {
 #define FD_KERN_CTAB     "fd_ed25519_ctab_init"
 #define FD_KERN_CBASE    "fd_ed25519_ctab_base"
 #define FD_KERN_LATTEST  "fd_ed25519_lattice_test_kernel"
+#define FD_KERN_FETEST   "fd_fe_test_kernel"
 #define FD_KERN_SHA512   "fd_sha512_batch_kernel"
 #define FD_KERN_KBUILD   "fd_ed25519_ktab_build_kernel"
 #define FD_KERN_KPART    "fd_ed25519_kcache_part_kernel"

@@ -1737,3 +1737,50 @@ extern "C" __global__ void fd_ed25519_lattice_test_kernel( uint32_t const * k, u
   }
 }
 
+
+/* Self-test kernel (tests only, fd_ed25519_gpu_test_field): the device field
+   and group operations on caller-supplied limbs, one operation per launch,
+   one input per lane (a, b: 40 limbs each; out: 40 limbs), so the tests can
+   hold the inline-asm device code limb for limb against the host build of
+   the same headers at the documented bounds.
+     0 fe_mul(a,b)  1 fe_sq(a)  2 fe_sq_neg(a)  3 fe_sq_seed(a,b)  4 fe_add(a,b)
+     5 fe_sub(a,b)  6 fe_lshl1_add(a,b)  7 fe_cneg(a, b[0]&1)
+     8 ge_dbl(a) with T  9 ge_add_cached(a, b) with T  (points: X,Y,Z,T limbs) */
+extern "C" __global__ void __launch_bounds__( 64 )
+fd_fe_test_kernel( int op, uint32_t const * a, uint32_t const * b, uint32_t * out, uint64_t n ) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  uint32_t const * pa = a + i*40u;
+  uint32_t const * pb = b + i*40u;
+  uint32_t * po = out + i*40u;
+  fe x, y, r;
+#pragma unroll
+  for( int j=0; j<10; j++ ) { x.v[j] = pa[j]; y.v[j] = pb[j]; r.v[j] = 0u; }
+  if( op <= 7 ) {
+    switch( op ) {
+      case 0: fe_mul( r, x, y ); break;
+      case 1: fe_sq( r, x ); break;
+      case 2: fe_sq_neg( r, x ); break;
+      case 3: fe_sq_seed( r, x, y ); break;
+      case 4: fe_add( r, x, y ); break;
+      case 5: fe_sub( r, x, y ); break;
+      case 6: fe_lshl1_add( r, x, y ); break;
+      default: fe_cneg( r, x, (pb[0] & 1u) != 0u ); break;
+    }
+#pragma unroll
+    for( int j=0; j<10; j++ ) po[j] = r.v[j];
+    return;
+  }
+  ge_p3 p, o;
+#pragma unroll
+  for( int j=0; j<10; j++ ) { p.X.v[j] = pa[j]; p.Y.v[j] = pa[10+j]; p.Z.v[j] = pa[20+j]; p.T.v[j] = pa[30+j]; }
+  if( op == 8 ) ge_dbl( o, p, true );
+  else {
+    ge_cached q;
+#pragma unroll
+    for( int j=0; j<10; j++ ) { q.YpX.v[j] = pb[j]; q.YmX.v[j] = pb[10+j]; q.T2d.v[j] = pb[20+j]; q.Z2.v[j] = pb[30+j]; }
+    ge_add_cached( o, p, q, true );
+  }
+#pragma unroll
+  for( int j=0; j<10; j++ ) { po[j] = o.X.v[j]; po[10+j] = o.Y.v[j]; po[20+j] = o.Z.v[j]; po[30+j] = o.T.v[j]; }
+}

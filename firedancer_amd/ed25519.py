@@ -85,6 +85,7 @@ def load_lib():
     lib.fd_ed25519_gpu_txn_reduce.restype = ctypes.c_int64
     lib.fd_ed25519_gpu_txn_reduce.argtypes = [vp, vp, u64, vp, u64]
     lib.fd_ed25519_gpu_test_lattice.argtypes = [vp, vp, u64, vp]
+    lib.fd_ed25519_gpu_test_field.argtypes = [vp, ctypes.c_int, vp, vp, u64, vp]
     lib.fd_sha512_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
     lib.fd_sha512_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
     lib.fd_sha256_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
@@ -382,6 +383,18 @@ class Ed25519Gpu:
         r = self.lib.fd_ed25519_gpu_test_lattice(self.ctx, _ptr(k_words), len(k_words), _ptr(out))
         if r:
             raise GpuError("fd_ed25519_gpu_test_lattice: %s (%d)" % (strerror(r), r))
+        return out
+
+    def test_field(self, op, a, b):
+        """Test hook: one device field / group operation (fd_ed25519_gpu_test_field)
+        on uint32 arrays a, b of shape [n, 40] -> uint32 array [n, 40]."""
+        a = np.ascontiguousarray(a, dtype=np.uint32)
+        b = np.ascontiguousarray(b, dtype=np.uint32)
+        assert a.shape == b.shape and a.ndim == 2 and a.shape[1] == 40, (a.shape, b.shape)
+        out = np.zeros_like(a)
+        r = self.lib.fd_ed25519_gpu_test_field(self.ctx, op, _ptr(a), _ptr(b), len(a), _ptr(out))
+        if r:
+            raise GpuError("fd_ed25519_gpu_test_field: %s (%d)" % (strerror(r), r))
         return out
 
     def keycache_reserve(self, capacity):

@@ -530,6 +530,16 @@ int fd_ed25519_gpu_test_ctab_stats( int dev, uint64_t * refs, uint64_t * builds 
    18 u32 = |u| (8), v (8), sign of u, iteration count. */
 int fd_ed25519_gpu_test_lattice( fd_ed25519_gpu_t * ctx, uint32_t const * k, uint64_t n, uint32_t * out );
 
+/* Test hook (not part of the reference interface): one device field / group
+   operation (firedancer_amd/csrc/fd_f25519_dev.h, fd_curve25519_dev.h) per
+   call on n inputs of 40 u32 limbs each (a, b; out: 40 limbs each), on the
+   context's first device.  op: 0 fe_mul, 1 fe_sq, 2 fe_sq_neg, 3 fe_sq_seed,
+   4 fe_add, 5 fe_sub, 6 fe_lshl1_add, 7 fe_cneg (negate iff b[0] odd),
+   8 ge_dbl with T, 9 ge_add_cached with T (points as X,Y,Z,T; b as the
+   cached Y+X, Y-X, 2dT, 2Z). */
+int fd_ed25519_gpu_test_field( fd_ed25519_gpu_t * ctx, int op, uint32_t const * a, uint32_t const * b, uint64_t n,
+                               uint32_t * out );
+
 #ifdef __cplusplus
 }
 #endif

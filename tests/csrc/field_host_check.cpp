@@ -50,3 +50,38 @@ void t_dbl( uint32_t * r, uint32_t const * p ) {
   for( int i=0;i<10;i++ ){ r[i]=o.X.v[i]; r[10+i]=o.Y.v[i]; r[20+i]=o.Z.v[i]; r[30+i]=o.T.v[i]; }
 }
 }
+extern "C" {
+/* The host build of fd_fe_test_kernel's operations (fd_ed25519_gpu_kern.hip):
+   same op numbers, same 40-limb records, for a limb-exact comparison. */
+void t_op( int op, uint32_t const * a, uint32_t const * b, uint32_t * out, uint64_t n ) {
+  for( uint64_t i=0; i<n; i++ ) {
+    uint32_t const * pa = a + i*40u; uint32_t const * pb = b + i*40u; uint32_t * po = out + i*40u;
+    for( int j=0; j<40; j++ ) po[j] = 0u;
+    fe x, y, r;
+    for( int j=0; j<10; j++ ) { x.v[j] = pa[j]; y.v[j] = pb[j]; r.v[j] = 0u; }
+    if( op <= 7 ) {
+      switch( op ) {
+        case 0: fe_mul( r, x, y ); break;
+        case 1: fe_sq( r, x ); break;
+        case 2: fe_sq_neg( r, x ); break;
+        case 3: fe_sq_seed( r, x, y ); break;
+        case 4: fe_add( r, x, y ); break;
+        case 5: fe_sub( r, x, y ); break;
+        case 6: fe_lshl1_add( r, x, y ); break;
+        default: fe_cneg( r, x, (pb[0] & 1u) != 0u ); break;
+      }
+      for( int j=0; j<10; j++ ) po[j] = r.v[j];
+      continue;
+    }
+    ge_p3 p, o;
+    for( int j=0; j<10; j++ ) { p.X.v[j] = pa[j]; p.Y.v[j] = pa[10+j]; p.Z.v[j] = pa[20+j]; p.T.v[j] = pa[30+j]; }
+    if( op == 8 ) ge_dbl( o, p, true );
+    else {
+      ge_cached q;
+      for( int j=0; j<10; j++ ) { q.YpX.v[j] = pb[j]; q.YmX.v[j] = pb[10+j]; q.T2d.v[j] = pb[20+j]; q.Z2.v[j] = pb[30+j]; }
+      ge_add_cached( o, p, q, true );
+    }
+    for( int j=0; j<10; j++ ) { po[j] = o.X.v[j]; po[10+j] = o.Y.v[j]; po[20+j] = o.Z.v[j]; po[30+j] = o.T.v[j]; }
+  }
+}
+}
