@@ -8,8 +8,8 @@
    most max_batch frags.  With nothing outstanding any available frags go at
    once; with batches outstanding the next is submitted when at least
    max_batch/2 frags wait -- so under load batches grow to max_batch and up
-   to three are in flight (the pipelined kernel runs one phase of each per
-   launch), and at low load latency stays at one batch: the stage finishes
+   to FD_ED25519_GPU_QUEUE_DEPTH are in flight (the pipelined kernel runs one
+   phase of three of them per launch, one launch queued behind), and at low load latency stays at one batch: the stage finishes
    a lone batch with drain launches as soon as the GPU is idle. */
 
 #include "../../include/fd_ed25519_gpu.h"
@@ -32,7 +32,7 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
   if( !off || !ctx || !tc || !max_batch ) return FD_ED25519_GPU_ERR_ARG;
   fd_ed25519_gpu_stage_t * st = fd_ed25519_gpu_stage_new( ctx, tc, max_batch, threads );
   if( !st ) return FD_ED25519_GPU_ERR_OOM;
-  enum { DEPTH = 3 };                /* the stage's batches in flight */
+  enum { DEPTH = FD_ED25519_GPU_QUEUE_DEPTH };   /* the stage's batches in flight */
   uint64_t q_seq[ DEPTH ], q_cnt[ DEPTH ];   /* outstanding batches, oldest first */
   int q = 0;
   uint64_t done = fd_verify_offload_done_seq( off );
@@ -40,7 +40,7 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
   int err = FD_ED25519_GPU_OK;
   uint8_t * dc = fd_verify_offload_dcache( off );
   uint64_t dsz = fd_verify_offload_dcache_sz( off );
-  /* Private snapshots of the frag records of the (up to three) batches in
+  /* Private snapshots of the frag records of the (up to DEPTH) batches in
      flight: the client can rewrite the shared ring at any time, so the stage
      parses (and bounds-checks against dsz) a copy it alone owns. */
   std::vector<fd_ed25519_gpu_frag_t> snap[ DEPTH ];

@@ -254,10 +254,12 @@ extern "C" int fd_ed25519_gpu_poll_block( fd_ed25519_gpu_t * ctx );
 extern "C" uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx );
 extern "C" int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n );
 
-/* Batches outstanding at once: three, the depth of the pipelined verify
-   kernel (fd_ed25519_gpu_submit / fd_ed25519_gpu_frags_submit take up to
-   three and finish each one two launches after its own). */
-#define FD_VS_DEPTH 3
+/* Batches outstanding at once: the pipelined verify kernel's three phases
+   plus one queued launch (fd_ed25519_gpu_submit / fd_ed25519_gpu_frags_submit
+   take FD_ED25519_GPU_QUEUE_DEPTH and finish each one two launches after its
+   own; with only three, every blocking poll waited for the launch just
+   submitted and the GPU idled through each replay). */
+#define FD_VS_DEPTH FD_ED25519_GPU_QUEUE_DEPTH
 
 struct vs_batch {
   int                            state = 0; /* 0 free, 1 parsed, 2 on the GPU, 3 GPU done / nothing to verify */

@@ -5,6 +5,10 @@ import os
 
 import numpy as np
 
+# FD_ED25519_GPU_QUEUE_DEPTH (include/fd_ed25519_gpu.h): batches in flight for submit / poll
+# and the verify stage
+QUEUE_DEPTH = 5
+
 FD_ED25519_SUCCESS = 0
 FD_ED25519_ERR_SIG = -1
 FD_ED25519_ERR_PUBKEY = -2
@@ -295,8 +299,9 @@ class Ed25519Gpu:
         return out
 
     def submit(self, arena, arena_sz, desc, out):
-        """fd_ed25519_gpu_submit: up to three batches in flight (the pipelined
-        kernel's depth); raises GpuError with ERR_BUSY on a fourth."""
+        """fd_ed25519_gpu_submit: up to QUEUE_DEPTH batches in flight (the
+        pipelined kernel's three phases + one queued launch); raises GpuError
+        with ERR_BUSY on one more."""
         r = self.lib.fd_ed25519_gpu_submit(self.ctx, _ptr(arena), arena_sz, _ptr(desc), len(desc), _ptr(out))
         if r:
             raise GpuError("fd_ed25519_gpu_submit: %s (%d)" % (strerror(r), r))

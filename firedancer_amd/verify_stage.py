@@ -106,7 +106,7 @@ class VerifyStage:
 
 
 class AsyncStage:
-    """fd_ed25519_gpu_stage_*: up to three batches in flight, completed in order;
+    """fd_ed25519_gpu_stage_*: up to QUEUE_DEPTH batches in flight, completed in order;
     frags parsed on the GPU by default (device_parse=False: on the host)."""
 
     def __init__(self, gpu, tcache, max_frags, threads=4, device_parse=True):

@@ -39,6 +39,13 @@ extern "C" {
    such batches with FD_ED25519_GPU_ERR_ARG before launching). */
 #define FD_ED25519_GPU_CODE_BAD_DESC (-128)
 
+/* Batches in flight at once for fd_ed25519_gpu_submit / _poll and the verify
+   stage: the pipelined kernel's three phases plus one launch queued behind
+   them, so that while the host waits for (and then replays) the oldest
+   batch, whose phase C ran in the launch two submits later, the GPU already
+   has the next launch to run. */
+#define FD_ED25519_GPU_QUEUE_DEPTH 5
+
 /* Infrastructure status (return values) */
 #define FD_ED25519_GPU_OK          (0)
 #define FD_ED25519_GPU_PENDING     (1)
@@ -133,8 +140,9 @@ int      fd_ed25519_gpu_keycache_clear  ( fd_ed25519_gpu_t * ctx );
 
 /* Asynchronous pair (wiredancer-style push model, src/wiredancer/c/wd_f1.h:71-112):
    submit copies the arena span the descriptors touch and the descriptors to
-   HBM on a copy stream and enqueues the kernels, and returns; up to three
-   batches are in flight (a fourth submit returns FD_ED25519_GPU_ERR_BUSY).
+   HBM on a copy stream and enqueues the kernels, and returns; up to
+   FD_ED25519_GPU_QUEUE_DEPTH batches are in flight (one more submit returns
+   FD_ED25519_GPU_ERR_BUSY).
    Batches of at most one wave per SIMD per device (256 x CUs signatures)
    take the pipelined kernel (fd_ed25519_gpu_pipe_dev below): each launch runs
    phase A of the new batch, B of the previous one and C of the one before,
@@ -327,10 +335,10 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
    starts the next batch's GPU work, then replays the tcache steps for the
    completed batch and fills its result / sig arrays -- and returns
    FD_ED25519_GPU_OK, or FD_ED25519_GPU_PENDING (block == 0 only).  At most
-   three batches are outstanding (submit returns FD_ED25519_GPU_ERR_BUSY on a
-   fourth): each goes to the GPU at submit, so the pipelined kernel runs one
-   phase of each per launch, and the host parse of batch k+1 and the replay
-   of batch k overlap the GPU.  Batches complete strictly in submission order, which keeps the
+   FD_ED25519_GPU_QUEUE_DEPTH batches are outstanding (one more submit
+   returns FD_ED25519_GPU_ERR_BUSY): each goes to the GPU at submit, so the
+   pipelined kernel runs one phase of each per launch with one launch queued
+   behind, and the host parse and replay overlap the GPU.  Batches complete strictly in submission order, which keeps the
    tile's frag order for the tcache.  The frag bytes and the result / sig
    arrays of a batch must stay valid until its poll returns OK.  The stage
    uses ctx's async pair: no other submit on ctx while batches are pending. */

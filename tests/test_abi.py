@@ -168,3 +168,13 @@ def test_txn_reduce_long_run_is_err_sig_not_an_error():
     t = lib.fd_ed25519_gpu_txn_reduce(codes.ctypes.data_as(ctypes.c_void_p), desc.ctypes.data_as(ctypes.c_void_p),
                                       len(desc), small.ctypes.data_as(ctypes.c_void_p), 1)
     assert t == 3 and small[0] == fa.FD_ED25519_ERR_SIG      # runs past out_cap are counted, not written
+
+
+def test_queue_depth_mirror_matches_header():
+    """firedancer_amd.QUEUE_DEPTH mirrors FD_ED25519_GPU_QUEUE_DEPTH: the pipelined
+    kernel's three phases plus one queued launch."""
+    import re
+    import firedancer_amd as fa
+    h = open(os.path.join(REPO, "include", "fd_ed25519_gpu.h")).read()
+    m = re.search(r"#define FD_ED25519_GPU_QUEUE_DEPTH (\d+)", h)
+    assert m and int(m.group(1)) == fa.QUEUE_DEPTH == 5

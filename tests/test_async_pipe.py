@@ -36,8 +36,8 @@ def _sets():
             recs[-900:], recs[100:1500], [recs[i] for i in rng.permutation(len(recs))]]
 
 
-def test_async_three_in_flight(gpu):
-    """Submit until BUSY (three in flight), complete the oldest, submit again:
+def test_async_queue_depth_in_flight(gpu):
+    """Submit until BUSY (QUEUE_DEPTH in flight), complete the oldest, submit again:
     batches of different sizes and contents, all pipelined."""
     batches = [_host(s) for s in _sets()]
     p0, o0 = gpu.launch_stats()
@@ -49,7 +49,7 @@ def test_async_three_in_flight(gpu):
                 gpu.submit(a, sz, d, out)
             except fa.GpuError as e:
                 assert "-104" in str(e)          # FD_ED25519_GPU_ERR_BUSY
-                assert gpu.pending() == 3
+                assert gpu.pending() == fa.QUEUE_DEPTH
                 break
             nxt += 1
         assert gpu.poll(block=True)

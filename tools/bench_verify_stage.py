@@ -95,7 +95,7 @@ def main():
         times.append(time.perf_counter() - t1)
     dt = float(np.mean(times))
     # the asynchronous stage with the frags parsed on the GPU: --async-batch
-    # frags per batch, three batches in flight (the pipelined kernel: one
+    # frags per batch, QUEUE_DEPTH batches in flight (the pipelined kernel: one
     # phase of each per launch), over the same stream; and the same with the
     # one-shot kernels (FD_ED25519_GPU_ASYNC_PIPE=0) for the A/B
     ab = args.async_batch
@@ -107,16 +107,22 @@ def main():
         ast = fa.AsyncStage(big, fa.TCache(), ab, threads=8, device_parse=True)
         res_a = np.zeros(len(frags), np.int8); sig_a = np.zeros(len(frags), np.uint64)
 
+        host = {"submit_s": 0.0, "poll_s": 0.0}
+
         def run_async():
             ast.tcache.reset()
             i = 0
             while i < len(fr) or ast.pending():
-                if i < len(fr) and ast.pending() < 3:
+                if i < len(fr) and ast.pending() < fa.QUEUE_DEPTH:
                     j = min(len(fr), i + ab)
+                    t = time.perf_counter()
                     ast.submit(arena, len(arena), fr[i:j], res_a[i:j], sig_a[i:j])
+                    host["submit_s"] += time.perf_counter() - t
                     i = j
                 else:
+                    t = time.perf_counter()
                     ast.poll(True)
+                    host["poll_s"] += time.perf_counter() - t
 
         def timed():
             run_async()
@@ -125,6 +131,8 @@ def main():
                 t1 = time.perf_counter(); run_async(); t.append(time.perf_counter() - t1)
             return float(np.mean(t))
         dt_a = timed()
+        runs = args.steps + 1
+        host_ms = {"submit_ms_per_run": host["submit_s"] / runs * 1e3, "poll_ms_per_run": host["poll_s"] / runs * 1e3}
         res_pageable = res_a.copy()
         # the same with the frag area page-locked (a tile's dcache workspace is
         # registered once: fd_ed25519_gpu_host_register)
@@ -135,9 +143,9 @@ def main():
         launches = big.launch_stats()
         ast.close(); big.close()
         os.environ.pop("FD_ED25519_GPU_ASYNC_PIPE", None)
-        return dt_a, dt_r, res_a, launches
-    dt_a, dt_r, res_a, launches = measure(True)
-    dt_o, dt_or, res_o, launches_o = measure(False)
+        return dt_a, dt_r, res_a, launches, host_ms
+    dt_a, dt_r, res_a, launches, host_a = measure(True)
+    dt_o, dt_or, res_o, launches_o, host_o = measure(False)
     assert np.array_equal(res_a, res_o)
     line = {"metric": "verify-stage frags/sec (fd_ed25519_gpu_verify_frags, host frags)",
             "value": args.frags / dt, "unit": "frags/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -147,7 +155,8 @@ def main():
                        "arena_bytes": int(len(arena))},
             "sigs_per_s": n_sigs / dt, "host_parse_ms": parse_ms, "results": hist, "gen_s": gen_s,
             "async_device_parse": {"frags_per_s": args.frags / dt_a, "ms": dt_a * 1e3, "batch": ab,
-                                   "in_flight": 3, "kernel": "pipelined", "launches_pipe_oneshot": launches,
+                                   "in_flight": fa.QUEUE_DEPTH, "kernel": "pipelined", "launches_pipe_oneshot": launches,
+                                   "host_calls": host_a,
                                    "registered_frags_per_s": args.frags / dt_r, "registered_ms": dt_r * 1e3,
                                    "sigs_per_s": n_sigs / dt_a, "registered_sigs_per_s": n_sigs / dt_r,
                                    "results": {int(k): int(v) for k, v in zip(*np.unique(res_a, return_counts=True))}},
