@@ -9,7 +9,7 @@
    once; with batches outstanding the next is submitted when at least
    max_batch/2 frags wait -- so under load batches grow to max_batch and up
    to FD_ED25519_GPU_QUEUE_DEPTH are in flight (the pipelined kernel runs one
-   phase of three of them per launch, one launch queued behind), and at low load latency stays at one batch: the stage finishes
+   phase of three of them per launch, two launches queued behind), and at low load latency stays at one batch: the stage finishes
    a lone batch with drain launches as soon as the GPU is idle. */
 
 #include "../../include/fd_ed25519_gpu.h"

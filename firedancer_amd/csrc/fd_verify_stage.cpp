@@ -255,7 +255,7 @@ extern "C" uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx );
 extern "C" int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n );
 
 /* Batches outstanding at once: the pipelined verify kernel's three phases
-   plus one queued launch (fd_ed25519_gpu_submit / fd_ed25519_gpu_frags_submit
+   plus two queued launches (fd_ed25519_gpu_submit / fd_ed25519_gpu_frags_submit
    take FD_ED25519_GPU_QUEUE_DEPTH and finish each one two launches after its
    own; with only three, every blocking poll waited for the launch just
    submitted and the GPU idled through each replay). */

@@ -300,7 +300,7 @@ class Ed25519Gpu:
 
     def submit(self, arena, arena_sz, desc, out):
         """fd_ed25519_gpu_submit: up to QUEUE_DEPTH batches in flight (the
-        pipelined kernel's three phases + one queued launch); raises GpuError
+        pipelined kernel's three phases + two queued launches); raises GpuError
         with ERR_BUSY on one more."""
         r = self.lib.fd_ed25519_gpu_submit(self.ctx, _ptr(arena), arena_sz, _ptr(desc), len(desc), _ptr(out))
         if r:

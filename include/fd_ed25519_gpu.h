@@ -40,10 +40,13 @@ extern "C" {
 #define FD_ED25519_GPU_CODE_BAD_DESC (-128)
 
 /* Batches in flight at once for fd_ed25519_gpu_submit / _poll and the verify
-   stage: the pipelined kernel's three phases plus one launch queued behind
+   stage: the pipelined kernel's three phases plus two launches queued behind
    them, so that while the host waits for (and then replays) the oldest
    batch, whose phase C ran in the launch two submits later, the GPU already
-   has the next launch to run. */
+   has the next launches to run, and a pageable batch's copy to HBM (staged
+   by the host inside submit) is issued a launch ahead of its use
+   (tools/bench_verify_stage.py: with three the GPU idled through every
+   replay, profiles/r03/stage_trace). */
 #define FD_ED25519_GPU_QUEUE_DEPTH 5
 
 /* Infrastructure status (return values) */

@@ -172,7 +172,7 @@ def test_txn_reduce_long_run_is_err_sig_not_an_error():
 
 def test_queue_depth_mirror_matches_header():
     """firedancer_amd.QUEUE_DEPTH mirrors FD_ED25519_GPU_QUEUE_DEPTH: the pipelined
-    kernel's three phases plus one queued launch."""
+    kernel's three phases plus two queued launches."""
     import re
     import firedancer_amd as fa
     h = open(os.path.join(REPO, "include", "fd_ed25519_gpu.h")).read()

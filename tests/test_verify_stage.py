@@ -324,7 +324,7 @@ def test_verify_frags_random_stream_vs_reference_tile(gpu, ref):
 def test_stage_async_queue_depth_vs_reference_tile(gpu, ref, devparse):
     """The asynchronous stage (fd_ed25519_gpu_stage_*): batches of varying
     size submitted with up to QUEUE_DEPTH outstanding (the pipelined kernel's
-    three phases + one queued launch), completed in order; results
+    three phases + two queued launches), completed in order; results
     equal the sequential reference tile's -- with the frags parsed on the GPU
     (default) and on the host."""
     import ctypes as C
