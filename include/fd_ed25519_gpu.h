@@ -340,7 +340,7 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
    FD_ED25519_GPU_OK, or FD_ED25519_GPU_PENDING (block == 0 only).  At most
    FD_ED25519_GPU_QUEUE_DEPTH batches are outstanding (one more submit
    returns FD_ED25519_GPU_ERR_BUSY): each goes to the GPU at submit, so the
-   pipelined kernel runs one phase of each per launch with one launch queued
+   pipelined kernel runs one phase of each per launch with two launches queued
    behind, and the host parse and replay overlap the GPU.  Batches complete strictly in submission order, which keeps the
    tile's frag order for the tcache.  The frag bytes and the result / sig
    arrays of a batch must stay valid until its poll returns OK.  The stage
