@@ -36,6 +36,28 @@
 #define STAMP( i ) do {} while( 0 )
 #endif
 
+/* ------------------------------------------------------------------ stores */
+
+/* Stores of data the NEXT launch reads (pipe hand-offs, partial sums) and of
+   the variable-base tables.  FD_NT_STORES / FD_NT_TABLES (A/B builds): with
+   the nontemporal policy. */
+typedef unsigned int fd_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_next( uint32_t * p, uint32_t v ) {
+#ifdef FD_NT_STORES
+  asm volatile( "global_store_dword %0, %1, off nt" :: "v"(p), "v"(v) : "memory" );
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void st_tab( uint4 * p, uint32_t x, uint32_t y, uint32_t z, uint32_t w ) {
+#ifdef FD_NT_TABLES
+  fd_u32x4 v = { x, y, z, w };
+  asm volatile( "global_store_dwordx4 %0, %1, off nt" :: "v"(p), "v"(v) : "memory" );
+#else
+  *p = make_uint4( x, y, z, w );
+#endif
+}
+
 /* ------------------------------------------------------------------ loads */
 
 /* n little-endian words starting at an arbitrary byte offset off (read
@@ -199,6 +221,14 @@ __device__ __forceinline__ void vtab_ptrs( uint32_t const * vtab, uint64_t cap, 
   }
 }
 
+/* Entry |d| of a biased digit db = d + 8 (db <= 16 by construction; clamped
+   to the table all the same): one v_sad_u32 (|db - 8| + 0) and a min. */
+__device__ __forceinline__ uint32_t vtab_entry( uint32_t db ) {
+  uint32_t e;
+  asm( "v_sad_u32 %0, %1, 8, 0" : "=v"(e) : "v"(db) );
+  return min( e, 8u );
+}
+
 __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint64_t t, int e, ge_cached const & c ) {
   uint32_t w[ 40 ];
 #pragma unroll
@@ -213,9 +243,9 @@ __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint6
   return;
 #endif
 #pragma unroll
-  for( int j=0; j<8; j++ ) m[j] = make_uint4( w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
+  for( int j=0; j<8; j++ ) st_tab( m + j, w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
 #pragma unroll
-  for( int j=0; j<2; j++ ) tl[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
+  for( int j=0; j<2; j++ ) st_tab( tl + j, w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
 }
 
 /* Table [0..8](-Q) for an affine Q (Z = 1), cached form (replaces the
@@ -235,12 +265,15 @@ __device__ __forceinline__ void vtab_build( uint32_t * vtab, uint64_t cap, uint6
   ge_dbl( P, nQ, true ); ge_to_cached( c, P ); vtab_store( vtab, cap, t, 2, c );
 #pragma unroll 1
   for( int e=3; e<=8; e++ ) { ge_madd( P, P, nQp, true ); ge_to_cached( c, P ); vtab_store( vtab, cap, t, e, c ); FE_FENCE(); }
+#ifdef FD_NT_TABLES
+  __builtin_amdgcn_s_waitcnt( 0x0f70 );      /* vmcnt(0): the table's stores done before any fetch of them */
+#endif
 }
 
 /* Issue the loads of entry |d| (biased digit db = d + 8) into raw words;
    vtab_finish (at the use point) applies the sign. */
 __device__ __forceinline__ void vtab_fetch( uint32_t w[ 40 ], uint32_t const * vtab, uint64_t cap, uint64_t t, uint32_t db ) {
-  uint32_t e = min( db < 8u ? 8u - db : db - 8u, 8u );
+  uint32_t e = vtab_entry( db );
   uint4 const * m; uint4 const * tl;
   vtab_ptrs( vtab, cap, t, e, &m, &tl );
 #pragma unroll
@@ -530,27 +563,43 @@ __device__ __forceinline__ int verify_tail( verify_args const & args, bool desc_
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+/* N 16-byte chunks of one per-lane record at g into the wave's LDS buffer
+   chunks buf[j][64] by LDS-DMA from ONE address: chunk j's 16 j bytes are
+   the instruction's immediate offset, which the DMA adds to the LDS address
+   as well, so its LDS base (M0) is taken 16 j bytes lower -- no address
+   arithmetic per chunk.  (The offset must be a constant: a template.) */
+template<int J, int N>
+__device__ __forceinline__ void glds_chunks( void const * g, uint4 * buf ) {
+  if constexpr( J < N ) {
+#ifdef FD_GLDS_NO_OFFSET   /* A/B build: an address per chunk, no immediate offset */
+    __builtin_amdgcn_global_load_lds( (char const *)g + 16*J, (lds_void_t *)(buf + 64*J), 16, 0, 0 );
+#else
+    __builtin_amdgcn_global_load_lds( g, (lds_void_t *)((char *)(buf + 64*J) - 16*J), 16, 16*J, 0 );
+#endif
+    glds_chunks<J+1, N>( g, buf );
+  }
+}
+template<int N>
+__device__ __forceinline__ void glds_record( void const * g, uint4 * buf ) { glds_chunks<0, N>( g, buf ); }
+
 /* One table entry (10 x 16 B per lane) into the wave's LDS buffer
    buf[10][64] by LDS-DMA. */
 __device__ __forceinline__ void vtab_fetch_lds( uint4 * buf, uint32_t const * vtab, uint64_t cap, uint64_t t, uint32_t db ) {
-  uint32_t e = min( db < 8u ? 8u - db : db - 8u, 8u );
+  uint32_t e = vtab_entry( db );
 #ifdef FD_DIAG_VTAB_ONE_ENTRY   /* diagnostic (wrong results): every fetch reads the shared identity record */
   e = 0u;
 #endif
   uint4 const * m; uint4 const * tl;
   vtab_ptrs( vtab, cap, t, e, &m, &tl );
-#pragma unroll
-  for( int j=0; j<8; j++ ) __builtin_amdgcn_global_load_lds( (void const *)(m + j), (lds_void_t *)(buf + 64*j), 16, 0, 0 );
-#pragma unroll
-  for( int j=0; j<2; j++ ) __builtin_amdgcn_global_load_lds( (void const *)(tl + j), (lds_void_t *)(buf + 64*(8+j)), 16, 0, 0 );
+  glds_record<8>( m, buf );
+  glds_record<2>( tl, buf + 64*8 );
 }
 
 /* Comb-table entry |d| of position k into buf[8][64]. */
 __device__ __forceinline__ void ctab_fetch_lds( uint4 * buf, uint32_t const * ctab, int k, int d ) {
   uint32_t e = min( (uint32_t)(d < 0 ? -d : d), FD_CTAB_HALF );
   uint4 const * p = (uint4 const *)(ctab + ((uint64_t)k * FD_CTAB_N + e) * FD_CTAB_STRIDE);
-#pragma unroll
-  for( int j=0; j<8; j++ ) __builtin_amdgcn_global_load_lds( (void const *)(p + j), (lds_void_t *)(buf + 64*j), 16, 0, 0 );
+  glds_record<8>( p, buf );
 }
 
 /* The wave's LDS-DMA has landed (this wave's only vector-memory operations
@@ -1121,19 +1170,19 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       uint32_t * h = a.hand_a + gid;
       uint32_t y[ 8 ];
 #pragma unroll
-      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_R + j)*cap ] = sig[j];
+      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_R + j)*cap, sig[j] );
       ybias4( y, u, nw );
 #pragma unroll
-      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YU + j)*cap ] = y[j];
+      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_YU + j)*cap, y[j] );
       ybias4( y, v, nw );
 #pragma unroll
-      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YV + j)*cap ] = y[j];
+      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_YV + j)*cap, y[j] );
       comb_bias( y, w );
 #pragma unroll
-      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YW + j)*cap ] = y[j];
+      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_YW + j)*cap, y[j] );
 #pragma unroll
-      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_A + j)*cap ] = pub[j];
-      h[ (uint64_t)FD_PH_IDX*cap ] = (uint32_t)di;
+      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_A + j)*cap, pub[j] );
+      st_next( h + (uint64_t)FD_PH_IDX*cap, (uint32_t)di );
     }
     if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)nw;
     FE_FENCE();
@@ -1159,10 +1208,14 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   uint32_t const * hand = phb ? a.hand_b : a.hand_c;
   int ps = gid < nx ? (int)(phb ? a.st_b : a.st_c)[ gid ] : 0;
   bool valid = (ps & FD_PIPE_ST_VALID) != 0;            /* phase A marked the batch's slots */
+  /* the status bits read after the decodes travel as wave ballots (SGPR
+     pairs): kept as the byte, ps was the kernel's one spilled VGPR */
+  uint64_t m_uneg = __ballot( (ps & FD_PIPE_ST_UNEG) != 0 );
+  uint64_t m_desc = __ballot( (ps & FD_PIPE_ST_DESC) != 0 ), m_bads = __ballot( (ps & FD_PIPE_ST_BADS) != 0 );
   if( !__ballot( valid ) ) return;                      /* a wave past a device-side count */
   int code;
   if( phb ) {
-    bool desc_ok = (ps & FD_PIPE_ST_DESC) != 0, bad_s = (ps & FD_PIPE_ST_BADS) != 0;
+    bool desc_ok = (m_desc >> lane) & 1u, bad_s = (m_bads >> lane) & 1u;
     int stA = 0, stR = 0;
     if( desc_ok && !bad_s ) {                         /* A: decode, small order, table */
       uint32_t enc[ 8 ];
@@ -1211,15 +1264,15 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
     }
     FE_FENCE();
     if( hi > lo )
-      chain_seg( acc, buf, y, y + 8*64, lane, (ps & FD_PIPE_ST_UNEG) != 0, args.vtab, vcap,
+      chain_seg( acc, buf, y, y + 8*64, lane, ((m_uneg >> lane) & 1u) != 0, args.vtab, vcap,
                  (2u*set)*cap + gid, (2u*set + 1u)*cap + gid, nw, hi, lo );
     FE_FENCE();
     if( phb ) {
       uint32_t * o = a.acc_b + gid;
 #pragma unroll
       for( int j=0; j<10; j++ ) {
-        o[ (uint64_t)j*cap ] = acc.X.v[j]; o[ (uint64_t)(10+j)*cap ] = acc.Y.v[j];
-        o[ (uint64_t)(20+j)*cap ] = acc.Z.v[j]; o[ (uint64_t)(30+j)*cap ] = acc.T.v[j];
+        st_next( o + (uint64_t)j*cap, acc.X.v[j] ); st_next( o + (uint64_t)(10+j)*cap, acc.Y.v[j] );
+        st_next( o + (uint64_t)(20+j)*cap, acc.Z.v[j] ); st_next( o + (uint64_t)(30+j)*cap, acc.T.v[j] );
       }
     } else {
       comb_lds( acc, buf, y + 16*64, lane, args.ctab );

@@ -110,17 +110,21 @@ FD_FN void fe_add( fe & r, fe const & a, fe const & b ) {
   for( int i=0; i<5; i++ ) FE_UNPK( r, i, pk_add( FE_PK( a, i ), FE_PK( b, i ) ) );
 }
 
-/* r = a + 2p - b.  Requires b limbs <= 2p limbs (b in R).  a + 2p as limb
-   pairs first (no limb goes negative), then the ten subtractions. */
-#define FE_2P_PK0 ( (uint64_t)FE_2P0 | ((uint64_t)FE_2PO << 32) )
-#define FE_2P_PK  ( (uint64_t)FE_2PE | ((uint64_t)FE_2PO << 32) )
+/* r = a + 2p - b.  Requires b limbs <= 2p limbs (b in R).  On the device
+   each limb is ONE v_sad_u32: |2p_i - b_i| + a_i, which is 2p_i - b_i + a_i
+   since b_i <= 2p_i (and every value is below 2^31, so the signed and the
+   unsigned readings of the difference agree) -- ten instructions instead of
+   five bias pair-adds plus ten subtractions. */
 FD_FN void fe_sub( fe & r, fe const & a, fe const & b ) {
-  fe t;
-  FE_UNPK( t, 0, pk_add_s( FE_PK( a, 0 ), FE_2P_PK0 ) );
 #pragma unroll
-  for( int i=1; i<5; i++ ) FE_UNPK( t, i, pk_add_s( FE_PK( a, i ), FE_2P_PK ) );
-#pragma unroll
-  for( int i=0; i<10; i++ ) r.v[i] = t.v[i] - b.v[i];
+  for( int i=0; i<10; i++ ) {
+    uint32_t c = i == 0 ? FE_2P0 : ((i & 1) ? FE_2PO : FE_2PE);
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm( "v_sad_u32 %0, %1, %2, %3" : "=v"(r.v[i]) : "s"(c), "v"(b.v[i]), "v"(a.v[i]) );
+#else
+    r.v[i] = c - b.v[i] + a.v[i];
+#endif
+  }
 }
 
 /* One parallel carry round: limbs < 2^31 in, R out. */

@@ -52,7 +52,7 @@ for _ in range(100):                       # clock ramp
         launch(k)
 torch.cuda.synchronize()
 times = [[] for _ in libs]
-for rnd in range(12):
+for rnd in range(int(__import__("os").environ.get("AB_ROUNDS", "12"))):
     for k in list(range(len(libs))) if rnd % 2 == 0 else list(reversed(range(len(libs)))):
         for _ in range(3):                 # this build's clock state before the sample
             launch(k)
