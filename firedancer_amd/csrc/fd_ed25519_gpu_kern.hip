@@ -36,28 +36,6 @@
 #define STAMP( i ) do {} while( 0 )
 #endif
 
-/* ------------------------------------------------------------------ stores */
-
-/* Stores of data the NEXT launch reads (pipe hand-offs, partial sums) and of
-   the variable-base tables.  FD_NT_STORES / FD_NT_TABLES (A/B builds): with
-   the nontemporal policy. */
-typedef unsigned int fd_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st_next( uint32_t * p, uint32_t v ) {
-#ifdef FD_NT_STORES
-  asm volatile( "global_store_dword %0, %1, off nt" :: "v"(p), "v"(v) : "memory" );
-#else
-  *p = v;
-#endif
-}
-__device__ __forceinline__ void st_tab( uint4 * p, uint32_t x, uint32_t y, uint32_t z, uint32_t w ) {
-#ifdef FD_NT_TABLES
-  fd_u32x4 v = { x, y, z, w };
-  asm volatile( "global_store_dwordx4 %0, %1, off nt" :: "v"(p), "v"(v) : "memory" );
-#else
-  *p = make_uint4( x, y, z, w );
-#endif
-}
-
 /* ------------------------------------------------------------------ loads */
 
 /* n little-endian words starting at an arbitrary byte offset off (read
@@ -243,9 +221,9 @@ __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint6
   return;
 #endif
 #pragma unroll
-  for( int j=0; j<8; j++ ) st_tab( m + j, w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
+  for( int j=0; j<8; j++ ) m[j] = make_uint4( w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
 #pragma unroll
-  for( int j=0; j<2; j++ ) st_tab( tl + j, w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
+  for( int j=0; j<2; j++ ) tl[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
 }
 
 /* Table [0..8](-Q) for an affine Q (Z = 1), cached form (replaces the
@@ -265,9 +243,6 @@ __device__ __forceinline__ void vtab_build( uint32_t * vtab, uint64_t cap, uint6
   ge_dbl( P, nQ, true ); ge_to_cached( c, P ); vtab_store( vtab, cap, t, 2, c );
 #pragma unroll 1
   for( int e=3; e<=8; e++ ) { ge_madd( P, P, nQp, true ); ge_to_cached( c, P ); vtab_store( vtab, cap, t, e, c ); FE_FENCE(); }
-#ifdef FD_NT_TABLES
-  __builtin_amdgcn_s_waitcnt( 0x0f70 );      /* vmcnt(0): the table's stores done before any fetch of them */
-#endif
 }
 
 /* Issue the loads of entry |d| (biased digit db = d + 8) into raw words;
@@ -571,11 +546,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 template<int J, int N>
 __device__ __forceinline__ void glds_chunks( void const * g, uint4 * buf ) {
   if constexpr( J < N ) {
-#ifdef FD_GLDS_NO_OFFSET   /* A/B build: an address per chunk, no immediate offset */
-    __builtin_amdgcn_global_load_lds( (char const *)g + 16*J, (lds_void_t *)(buf + 64*J), 16, 0, 0 );
-#else
     __builtin_amdgcn_global_load_lds( g, (lds_void_t *)((char *)(buf + 64*J) - 16*J), 16, 16*J, 0 );
-#endif
     glds_chunks<J+1, N>( g, buf );
   }
 }
@@ -1170,19 +1141,19 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       uint32_t * h = a.hand_a + gid;
       uint32_t y[ 8 ];
 #pragma unroll
-      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_R + j)*cap, sig[j] );
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_R + j)*cap ] = sig[j];
       ybias4( y, u, nw );
 #pragma unroll
-      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_YU + j)*cap, y[j] );
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YU + j)*cap ] = y[j];
       ybias4( y, v, nw );
 #pragma unroll
-      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_YV + j)*cap, y[j] );
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YV + j)*cap ] = y[j];
       comb_bias( y, w );
 #pragma unroll
-      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_YW + j)*cap, y[j] );
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YW + j)*cap ] = y[j];
 #pragma unroll
-      for( int j=0; j<8; j++ ) st_next( h + (uint64_t)(FD_PH_A + j)*cap, pub[j] );
-      st_next( h + (uint64_t)FD_PH_IDX*cap, (uint32_t)di );
+      for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_A + j)*cap ] = pub[j];
+      h[ (uint64_t)FD_PH_IDX*cap ] = (uint32_t)di;
     }
     if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)nw;
     FE_FENCE();
@@ -1271,8 +1242,8 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       uint32_t * o = a.acc_b + gid;
 #pragma unroll
       for( int j=0; j<10; j++ ) {
-        st_next( o + (uint64_t)j*cap, acc.X.v[j] ); st_next( o + (uint64_t)(10+j)*cap, acc.Y.v[j] );
-        st_next( o + (uint64_t)(20+j)*cap, acc.Z.v[j] ); st_next( o + (uint64_t)(30+j)*cap, acc.T.v[j] );
+        o[ (uint64_t)j*cap ] = acc.X.v[j]; o[ (uint64_t)(10+j)*cap ] = acc.Y.v[j];
+        o[ (uint64_t)(20+j)*cap ] = acc.Z.v[j]; o[ (uint64_t)(30+j)*cap ] = acc.T.v[j];
       }
     } else {
       comb_lds( acc, buf, y + 16*64, lane, args.ctab );
