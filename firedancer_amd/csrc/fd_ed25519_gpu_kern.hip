@@ -627,6 +627,22 @@ __device__ __forceinline__ uint32_t ydig( uint32_t const * y, int lane, int i, i
   return neg ? 16u - db : db;
 }
 
+/* The same for the recoding of ybias_p (wave-uniform top position P): window
+   nw-2 is wn = P - 4 (nw-2) bits wide (1..4; 4 is ydig's recoding), the top
+   digit sits at bit P (it may straddle two words). */
+__device__ __forceinline__ uint32_t ydig_p( uint32_t const * y, int lane, int i, int nw, int wn, bool neg ) {
+  uint32_t db;
+  if( i == nw-1 ) {
+    int P = 4*(nw-2) + wn, q = P >> 5;
+    uint64_t two = (uint64_t)y[ q*64 + lane ] | (q < 7 ? (uint64_t)y[ (q+1)*64 + lane ] << 32 : 0ull);
+    db = ((uint32_t)(two >> (P & 31)) & 15u) + 8u;         /* the top digit (<= 8) */
+  } else {
+    db = (y[ (i >> 3)*64 + lane ] >> (4*(i & 7))) & 15u;
+    if( i == nw-2 ) db = (db & ((1u << wn) - 1u)) + 8u - (1u << (wn - 1));
+  }
+  return neg ? 16u - db : db;
+}
+
 /* x + 8 (16^0 + ... + 16^(nw-2)): the signed 4-bit recoding of x < 2^(4 nw - 1)
    as a bias (digit i = nibble i - 8, the top one unbiased: recode4_lds). */
 __device__ __forceinline__ void ybias4( uint32_t y[ 8 ], uint32_t const x[ 8 ], int nw ) {
@@ -640,6 +656,34 @@ __device__ __forceinline__ void ybias4( uint32_t y[ 8 ], uint32_t const x[ 8 ], 
   }
 }
 
+/* The pipe kernel's recoding: the top digit at bit P (wave-uniform; P =
+   nbits - 3 for the wave's longest scalar, at least 124) instead of at
+   4 (nw-1), so the chain takes P doublings instead of 4 (nw-1): windows
+   0 .. m-2 are 4-bit (bias 8 each), window m-1 = nw-2 is wn = P - 4 (m-1)
+   bits (bias 2^(wn-1)), the top digit is y >> P; m = ceil(P / 4), nw = m + 1.
+   x < 2^(P+3) keeps the top digit <= 8 (y < 8.77 2^P; pinned on the CPU by
+   tests/test_field_bounds.py::test_pipe_recoding). */
+__device__ __forceinline__ void ybias_p( uint32_t y[ 8 ], uint32_t const x[ 8 ], int P ) {
+  int m = (P + 3) >> 2, wn = P - 4*(m - 1), eb = 4*(m - 1) + wn - 1;
+  uint64_t c = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) {
+    int nb = m - 1 - 8*j;                           /* 4-bit biased nibbles in word j */
+    uint32_t pat = nb >= 8 ? 0x88888888u : (nb <= 0 ? 0u : (0x88888888u & ((1u << (4*nb)) - 1u)));
+    uint32_t ex = (eb >> 5) == j ? (1u << (eb & 31)) : 0u;
+    c += (uint64_t)x[j] + pat + ex;
+    y[j] = (uint32_t)c; c >>= 32;
+  }
+}
+
+/* The pipe's top-digit position for the wave (its longest scalar has nbits
+   bits): P = nbits - 3, within [124, 252]. */
+__device__ __forceinline__ int wave_top_pos( int nbits ) {
+#pragma unroll
+  for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
+  return min( 4*(FD_NDIG_MAX-2) + 4, max( 124, nbits - 3 ) );
+}
+
 
 /* Windows hi-1 .. lo of the Straus chain acc = [u](-A) + [v](-R) (dsm_loop's
    order: four doublings unless it is the chain's first window, then A's and
@@ -648,14 +692,15 @@ __device__ __forceinline__ void ybias4( uint32_t y[ 8 ], uint32_t const x[ 8 ], 
    comb). */
 __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t const * yu, uint32_t const * yv, int lane,
                                            bool uneg, uint32_t const * vtab, uint64_t cap, uint64_t ta, uint64_t tr,
-                                           int nw, int hi, int lo ) {
-  uint32_t dba = ydig( yu, lane, hi-1, nw, uneg );
+                                           int nw, int hi, int lo, int wn = 4 ) {
+  uint32_t dba = ydig_p( yu, lane, hi-1, nw, wn, uneg );
   vtab_fetch_lds( buf, vtab, cap, ta, dba );
 #pragma unroll 1
   for( int i=hi-1; i>=lo; i-- ) {
     if( i < nw-1 ) {
+      int nd = i == nw-2 ? wn : 4;                  /* window nw-2 is wn bits wide (ybias_p) */
 #pragma unroll 1
-      for( int j=0; j<3; j++ ) { ge_dbl( acc, acc, false ); FE_FENCE(); }
+      for( int j=1; j<nd; j++ ) { ge_dbl( acc, acc, false ); FE_FENCE(); }
       ge_dbl( acc, acc, true );
       FE_FENCE();
     }
@@ -665,7 +710,7 @@ __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t co
       dma_wait();
       uint32_t w[ 40 ];
       lds_entry_words<10>( w, buf, lane, dba < 8u );
-      dbr = ydig( yv, lane, i, nw, false );
+      dbr = ydig_p( yv, lane, i, nw, wn, false );
       FE_FENCE();
       vtab_fetch_lds( buf, vtab, cap, tr, dbr );     /* LDS reads issued before the DMA see the old bytes */
       lds_entry_finish( q, w, dba < 8u );
@@ -677,7 +722,7 @@ __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t co
       dma_wait();
       uint32_t w[ 40 ];
       lds_entry_words<10>( w, buf, lane, dbr < 8u );
-      if( i > lo ) dba = ydig( yu, lane, i-1, nw, uneg );
+      if( i > lo ) dba = ydig_p( yu, lane, i-1, nw, wn, uneg );
       FE_FENCE();
       if( i > lo ) vtab_fetch_lds( buf, vtab, cap, ta, dba );
       lds_entry_finish( q, w, dbr < 8u );
@@ -1136,16 +1181,16 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #endif
                                     );
     FE_FENCE();
-    int nw = wave_windows( nbits );
+    int P = wave_top_pos( nbits );                  /* the chain's doublings (ybias_p) */
     if( valid ) {
       uint32_t * h = a.hand_a + gid;
       uint32_t y[ 8 ];
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_R + j)*cap ] = sig[j];
-      ybias4( y, u, nw );
+      ybias_p( y, u, P );
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YU + j)*cap ] = y[j];
-      ybias4( y, v, nw );
+      ybias_p( y, v, P );
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_YV + j)*cap ] = y[j];
       comb_bias( y, w );
@@ -1155,7 +1200,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_A + j)*cap ] = pub[j];
       h[ (uint64_t)FD_PH_IDX*cap ] = (uint32_t)di;
     }
-    if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)nw;
+    if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)P;     /* the wave's top-digit position */
     FE_FENCE();
     if( gid < args.n )
       a.st_a[ gid ] = !valid ? (uint8_t)0 : (uint8_t)(FD_PIPE_ST_VALID | (desc_ok ? FD_PIPE_ST_DESC : 0) | (bad_s ? FD_PIPE_ST_BADS : 0) |
@@ -1218,7 +1263,8 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
     code = valid ? (int)a.code_c[ gid ] : 0;
   }
   bool run = valid && code == 0;
-  int nw = __builtin_amdgcn_readfirstlane( (int)(phb ? a.nw_b : a.nw_c)[ gid >> 6 ] );
+  int P = __builtin_amdgcn_readfirstlane( (int)(phb ? a.nw_b : a.nw_c)[ gid >> 6 ] );
+  int nw = ((P + 3) >> 2) + 1, wn = P - 4*(nw - 2);    /* ybias_p's windows */
   int split = max( nw - (int)a.kb, 0 );
   int hi = phb ? nw : split, lo = phb ? split : 0;
   ge_p3 acc;
@@ -1236,7 +1282,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
     FE_FENCE();
     if( hi > lo )
       chain_seg( acc, buf, y, y + 8*64, lane, ((m_uneg >> lane) & 1u) != 0, args.vtab, vcap,
-                 (2u*set)*cap + gid, (2u*set + 1u)*cap + gid, nw, hi, lo );
+                 (2u*set)*cap + gid, (2u*set + 1u)*cap + gid, nw, hi, lo, wn );
     FE_FENCE();
     if( phb ) {
       uint32_t * o = a.acc_b + gid;
