@@ -307,7 +307,7 @@ __device__ __forceinline__ int wdig( uint8_t const * dig, int k ) {
    the last window. */
 template<bool COMB>
 __device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, uint64_t cap, uint64_t ta, uint64_t tr,
-                                          uint8_t const * dig, uint32_t const * ctab, int nw ) {
+                                          uint8_t const * dig, uint32_t const * ctab, int nw, int wn ) {
   ge_identity( acc );
   uint32_t raw[ 40 ];
   uint32_t craw[ 32 ];
@@ -317,9 +317,11 @@ __device__ __forceinline__ void dsm_loop( ge_p3 & acc, uint32_t const * vtab, ui
   for( int i=nw-1; i>=0; i-- ) {
     if( i < nw-1 ) {
       /* T only on the last doubling (the adds need it); a runtime want_t in
-         a rolled loop would compute it on all four */
+         a rolled loop would compute it on all four.  Window nw-2 is wn bits
+         wide (recode_p_lds) */
+      int nd = i == nw-2 ? wn : 4;
 #pragma unroll 1
-      for( int j=0; j<3; j++ ) { ge_dbl( acc, acc, false ); FE_FENCE(); }
+      for( int j=1; j<nd; j++ ) { ge_dbl( acc, acc, false ); FE_FENCE(); }
       ge_dbl( acc, acc, true );
       FE_FENCE();
     }
@@ -373,18 +375,55 @@ __device__ __forceinline__ int bitlen8( uint32_t const x[ 8 ] ) {
   return b;
 }
 
-/* Signed 4-bit recoding of x (< 2^(4 nw - 1)) into nw LDS rows (biased by 8,
-   negated when neg): digits in [-8, 7] below the top one, top digit in
-   [0, 8] (its top nibble <= 7 plus the incoming carry, never wrapped). */
-__device__ __forceinline__ void recode4_lds( uint8_t * row, uint32_t const x[ 8 ], int neg, int nw, uint64_t stride ) {
-  int c = 0;
+
+/* The pipe kernel's recoding: the top digit at bit P (wave-uniform; P =
+   nbits - 3 for the wave's longest scalar, at least 124) instead of at
+   4 (nw-1), so the chain takes P doublings instead of 4 (nw-1): windows
+   0 .. m-2 are 4-bit (bias 8 each), window m-1 = nw-2 is wn = P - 4 (m-1)
+   bits (bias 2^(wn-1)), the top digit is y >> P; m = ceil(P / 4), nw = m + 1.
+   x < 2^(P+3) keeps the top digit <= 8 (y < 8.77 2^P; pinned on the CPU by
+   tests/test_field_bounds.py::test_pipe_recoding). */
+__device__ __forceinline__ void ybias_p( uint32_t y[ 8 ], uint32_t const x[ 8 ], int P ) {
+  int m = (P + 3) >> 2, wn = P - 4*(m - 1), eb = 4*(m - 1) + wn - 1;
+  uint64_t c = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) {
+    int nb = m - 1 - 8*j;                           /* 4-bit biased nibbles in word j */
+    uint32_t pat = nb >= 8 ? 0x88888888u : (nb <= 0 ? 0u : (0x88888888u & ((1u << (4*nb)) - 1u)));
+    uint32_t ex = (eb >> 5) == j ? (1u << (eb & 31)) : 0u;
+    c += (uint64_t)x[j] + pat + ex;
+    y[j] = (uint32_t)c; c >>= 32;
+  }
+}
+
+/* The pipe's top-digit position for the wave (its longest scalar has nbits
+   bits): P = nbits - 3, within [124, 252]. */
+__device__ __forceinline__ int wave_top_pos( int nbits ) {
+#pragma unroll
+  for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
+  return min( 4*(FD_NDIG_MAX-2) + 4, max( 124, nbits - 3 ) );
+}
+
+/* recode_p_lds: ybias_p's digits into nw LDS byte rows (biased by 8, negated
+   when neg) for the one-shot kernels' Straus loop (dsm_loop): windows
+   0 .. nw-3 4-bit, window nw-2 wn bits, the top digit at bit P. */
+__device__ __forceinline__ void recode_p_lds( uint8_t * row, uint32_t const x[ 8 ], int neg, int P, uint64_t stride ) {
+  uint32_t y[ 8 ];
+  ybias_p( y, x, P );
+  int nw = ((P + 3) >> 2) + 1, wn = P - 4*(nw - 2);
 #pragma unroll
   for( int i=0; i<FD_NDIG_MAX; i++ ) {
     if( i < nw ) {
-      int d = (int)((x[i>>3] >> (4*(i&7))) & 15u) + c;
-      c = d >= 8 && i < nw-1;           /* the top digit keeps its carry: d in [0, 8] */
-      d -= c << 4;
-      row[ (uint64_t)i*stride ] = (uint8_t)((neg ? -d : d) + 8);
+      uint32_t db;
+      if( i == nw-1 ) {                              /* the top digit: bit P = 4 (i-1) + wn */
+        int j = i - 1 < 0 ? 0 : i - 1;
+        uint64_t two = (uint64_t)y[ j >> 3 ] | ((j >> 3) < 7 ? (uint64_t)y[ (j >> 3) + 1 ] << 32 : 0ull);
+        db = ((uint32_t)(two >> (4*(j & 7) + wn)) & 15u) + 8u;
+      } else {
+        db = (y[ i >> 3 ] >> (4*(i & 7))) & 15u;
+        if( i == nw-2 ) db = (db & ((1u << wn) - 1u)) + 8u - (1u << (wn - 1));
+      }
+      row[ (uint64_t)i*stride ] = (uint8_t)(neg ? 16u - db : db);
     }
   }
 }
@@ -419,17 +458,11 @@ __device__ __forceinline__ void verify_prep_scalars( uint32_t u[ 8 ], uint32_t v
   *nbits = max( bitlen8( u ), bitlen8( v ) );
 }
 
-/* The wave-uniform window count: x < 2^(4 nw - 1) for every lane's u, v. */
-__device__ __forceinline__ int wave_windows( int nbits ) {
-#pragma unroll
-  for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
-  return min( FD_NDIG_MAX, max( 32, (nbits + 4) >> 2 ) );
-}
 
 /* k, the lattice vector, w = v S mod l and their digits into this lane's
    column drow (rows FD_ROW_U / _V / _W, row r at drow[r * stride], LDS with
-   stride FD_VERIFY_BLOCK; FD_ROW_NW: the wave-uniform window count, written
-   by lane 0 of each wave).  Lanes that are not live write zero digits (every
+   stride FD_VERIFY_BLOCK; FD_ROW_NW: the wave-uniform top-digit position P
+   of recode_p_lds, written by lane 0 of each wave).  Lanes that are not live write zero digits (every
    lane takes part in the wave max). */
 __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, uint64_t stride, int tid, bool live, uint32_t const sig[ 16 ],
                                                     uint32_t const pub[ 8 ], verify_args const & args,
@@ -460,10 +493,10 @@ __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, uint64_t str
       drow[ (uint64_t)(FD_ROW_W + 3*k + 2)*stride ] = (uint8_t)((dd >> 16) & 255);
     }
   }
-  int nw = wave_windows( nbits );
-  recode4_lds( drow + FD_ROW_U*stride, u, un, nw, stride );
-  recode4_lds( drow + FD_ROW_V*stride, v, 0,  nw, stride );
-  if( (tid & 63) == 0 ) drow[ FD_ROW_NW*stride ] = (uint8_t)nw;
+  int P = wave_top_pos( nbits );
+  recode_p_lds( drow + FD_ROW_U*stride, u, un, P, stride );
+  recode_p_lds( drow + FD_ROW_V*stride, v, 0,  P, stride );
+  if( (tid & 63) == 0 ) drow[ FD_ROW_NW*stride ] = (uint8_t)P;     /* the wave's top-digit position */
 }
 
 /* The verify code from the check results, in the reference's order
@@ -492,11 +525,12 @@ __device__ __forceinline__ int verify_equation( verify_args const & args, uint8_
 #endif
                                                 ) {
   uint64_t cap = args.vtab_cap;
-  int nw = s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ];
+  int P = __builtin_amdgcn_readfirstlane( (int)s_dig[ FD_ROW_NW*FD_VERIFY_BLOCK + (tid & ~63) ] );
+  int nw = ((P + 3) >> 2) + 1, wn = P - 4*(nw - 2);  /* recode_p_lds's windows */
   ge_p3 acc;
-  if( !s_wb ) dsm_loop<true>( acc, args.vtab, cap, ta, tr, drow, args.ctab, nw );
+  if( !s_wb ) dsm_loop<true>( acc, args.vtab, cap, ta, tr, drow, args.ctab, nw, wn );
   else {
-    dsm_loop<false>( acc, args.vtab, cap, ta, tr, drow, args.ctab, nw );
+    dsm_loop<false>( acc, args.vtab, cap, ta, tr, drow, args.ctab, nw, wn );
     ge_cached c;
 #pragma unroll
     for( int j=0; j<10; j++ ) {
@@ -618,18 +652,11 @@ __device__ __forceinline__ void lds_entry_finish( ge_cached & c, uint32_t const 
   fe_cneg( c.T2d, tv, neg );
 }
 
-/* Biased 4-bit digit i (0..16) of a recoded scalar y = x + 8 (16^0 + ... +
-   16^(nw-2)) held in the wave's LDS column block y[8][64]: nibble i is
-   d_i + 8 below the top window and d_i at the top one (recode4_lds's
-   digits, read off the bits), negated when neg. */
-__device__ __forceinline__ uint32_t ydig( uint32_t const * y, int lane, int i, int nw, bool neg ) {
-  uint32_t db = ((y[ (i >> 3)*64 + lane ] >> (4*(i & 7))) & 15u) + (i == nw-1 ? 8u : 0u);
-  return neg ? 16u - db : db;
-}
-
-/* The same for the recoding of ybias_p (wave-uniform top position P): window
-   nw-2 is wn = P - 4 (nw-2) bits wide (1..4; 4 is ydig's recoding), the top
-   digit sits at bit P (it may straddle two words). */
+/* Biased digit i (0..16, d_i + 8) of a scalar recoded by ybias_p, held in
+   the wave's LDS column block y[8][64] (wave-uniform top position P = 4 (nw-2)
+   + wn): windows below nw-2 are nibbles biased by 8, window nw-2 is wn bits
+   (1..4) biased by 2^(wn-1), the top digit sits at bit P (it may straddle
+   two words); negated when neg. */
 __device__ __forceinline__ uint32_t ydig_p( uint32_t const * y, int lane, int i, int nw, int wn, bool neg ) {
   uint32_t db;
   if( i == nw-1 ) {
@@ -643,48 +670,6 @@ __device__ __forceinline__ uint32_t ydig_p( uint32_t const * y, int lane, int i,
   return neg ? 16u - db : db;
 }
 
-/* x + 8 (16^0 + ... + 16^(nw-2)): the signed 4-bit recoding of x < 2^(4 nw - 1)
-   as a bias (digit i = nibble i - 8, the top one unbiased: recode4_lds). */
-__device__ __forceinline__ void ybias4( uint32_t y[ 8 ], uint32_t const x[ 8 ], int nw ) {
-  uint64_t c = 0;
-#pragma unroll
-  for( int j=0; j<8; j++ ) {
-    int nb = nw - 1 - 8*j;                          /* biased nibbles in word j */
-    uint32_t pat = nb >= 8 ? 0x88888888u : (nb <= 0 ? 0u : (0x88888888u & ((1u << (4*nb)) - 1u)));
-    c += (uint64_t)x[j] + pat;
-    y[j] = (uint32_t)c; c >>= 32;
-  }
-}
-
-/* The pipe kernel's recoding: the top digit at bit P (wave-uniform; P =
-   nbits - 3 for the wave's longest scalar, at least 124) instead of at
-   4 (nw-1), so the chain takes P doublings instead of 4 (nw-1): windows
-   0 .. m-2 are 4-bit (bias 8 each), window m-1 = nw-2 is wn = P - 4 (m-1)
-   bits (bias 2^(wn-1)), the top digit is y >> P; m = ceil(P / 4), nw = m + 1.
-   x < 2^(P+3) keeps the top digit <= 8 (y < 8.77 2^P; pinned on the CPU by
-   tests/test_field_bounds.py::test_pipe_recoding). */
-__device__ __forceinline__ void ybias_p( uint32_t y[ 8 ], uint32_t const x[ 8 ], int P ) {
-  int m = (P + 3) >> 2, wn = P - 4*(m - 1), eb = 4*(m - 1) + wn - 1;
-  uint64_t c = 0;
-#pragma unroll
-  for( int j=0; j<8; j++ ) {
-    int nb = m - 1 - 8*j;                           /* 4-bit biased nibbles in word j */
-    uint32_t pat = nb >= 8 ? 0x88888888u : (nb <= 0 ? 0u : (0x88888888u & ((1u << (4*nb)) - 1u)));
-    uint32_t ex = (eb >> 5) == j ? (1u << (eb & 31)) : 0u;
-    c += (uint64_t)x[j] + pat + ex;
-    y[j] = (uint32_t)c; c >>= 32;
-  }
-}
-
-/* The pipe's top-digit position for the wave (its longest scalar has nbits
-   bits): P = nbits - 3, within [124, 252]. */
-__device__ __forceinline__ int wave_top_pos( int nbits ) {
-#pragma unroll
-  for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
-  return min( 4*(FD_NDIG_MAX-2) + 4, max( 124, nbits - 3 ) );
-}
-
-
 /* Windows hi-1 .. lo of the Straus chain acc = [u](-A) + [v](-R) (dsm_loop's
    order: four doublings unless it is the chain's first window, then A's and
    R's entries); entries staged in buf one addition ahead; T computed at the
@@ -692,7 +677,7 @@ __device__ __forceinline__ int wave_top_pos( int nbits ) {
    comb). */
 __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t const * yu, uint32_t const * yv, int lane,
                                            bool uneg, uint32_t const * vtab, uint64_t cap, uint64_t ta, uint64_t tr,
-                                           int nw, int hi, int lo, int wn = 4 ) {
+                                           int nw, int hi, int lo, int wn ) {
   uint32_t dba = ydig_p( yu, lane, hi-1, nw, wn, uneg );
   vtab_fetch_lds( buf, vtab, cap, ta, dba );
 #pragma unroll 1
@@ -816,7 +801,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
   /* k, the lattice vector (u, v), w; their biased digits into this lane's
      LDS column (before the decodes: only they and the sign of u stay live) */
   uint32_t * y = s_y[ wv ];
-  int un = 0, nwin = 32;
+  int un = 0, nwin = 124;          /* the top-digit position P (ybias_p) */
   {
     uint32_t u[ 8 ], v[ 8 ], w[ 8 ];
     int nbits = 0;
@@ -827,18 +812,18 @@ fd_ed25519_verify_kernel( verify_args args ) {
                                     , _st
 #endif
                                     );
-    int nw = wave_windows( nbits );
+    int P = wave_top_pos( nbits );                  /* the chain's doublings (ybias_p) */
     uint32_t t[ 8 ];
-    ybias4( t, u, nw );
+    ybias_p( t, u, P );
 #pragma unroll
     for( int j=0; j<8; j++ ) y[ j*64 + lane ] = t[j];
-    ybias4( t, v, nw );
+    ybias_p( t, v, P );
 #pragma unroll
     for( int j=0; j<8; j++ ) y[ (8 + j)*64 + lane ] = t[j];
     comb_bias( t, w );
 #pragma unroll
     for( int j=0; j<8; j++ ) y[ (16 + j)*64 + lane ] = t[j];
-    nwin = nw;
+    nwin = P;
   }
   FE_FENCE();
 
@@ -873,9 +858,10 @@ fd_ed25519_verify_kernel( verify_args args ) {
   int code = verify_precode( args, desc_ok, bad_s, stA, stR );
   if( code == 0 ) {
     /* Q = [u](-A) + [v](-R) + [w]B, Q == O  (:225-228 on [v]D) */
-    int nw = __builtin_amdgcn_readfirstlane( nwin );
+    int P = __builtin_amdgcn_readfirstlane( nwin );
+    int nw = ((P + 3) >> 2) + 1, wn = P - 4*(nw - 2);  /* ybias_p's windows */
     ge_p3 acc; ge_identity( acc );
-    chain_seg( acc, s_buf[ wv ], y, y + 8*64, lane, un != 0, args.vtab, cap, gid, cap/2u + gid, nw, nw, 0 );
+    chain_seg( acc, s_buf[ wv ], y, y + 8*64, lane, un != 0, args.vtab, cap, gid, cap/2u + gid, nw, nw, 0, wn );
     comb_lds( acc, s_buf[ wv ], y + 16*64, lane, args.ctab );
     STAMP( 5 );
     fe dl;
