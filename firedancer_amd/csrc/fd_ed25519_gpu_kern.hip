@@ -376,32 +376,12 @@ __device__ __forceinline__ int bitlen8( uint32_t const x[ 8 ] ) {
 }
 
 
-/* The pipe kernel's recoding: the top digit at bit P (wave-uniform; P =
-   nbits - 3 for the wave's longest scalar, at least 124) instead of at
-   4 (nw-1), so the chain takes P doublings instead of 4 (nw-1): windows
-   0 .. m-2 are 4-bit (bias 8 each), window m-1 = nw-2 is wn = P - 4 (m-1)
-   bits (bias 2^(wn-1)), the top digit is y >> P; m = ceil(P / 4), nw = m + 1.
-   x < 2^(P+3) keeps the top digit <= 8 (y < 8.77 2^P; pinned on the CPU by
-   tests/test_field_bounds.py::test_pipe_recoding). */
-__device__ __forceinline__ void ybias_p( uint32_t y[ 8 ], uint32_t const x[ 8 ], int P ) {
-  int m = (P + 3) >> 2, wn = P - 4*(m - 1), eb = 4*(m - 1) + wn - 1;
-  uint64_t c = 0;
-#pragma unroll
-  for( int j=0; j<8; j++ ) {
-    int nb = m - 1 - 8*j;                           /* 4-bit biased nibbles in word j */
-    uint32_t pat = nb >= 8 ? 0x88888888u : (nb <= 0 ? 0u : (0x88888888u & ((1u << (4*nb)) - 1u)));
-    uint32_t ex = (eb >> 5) == j ? (1u << (eb & 31)) : 0u;
-    c += (uint64_t)x[j] + pat + ex;
-    y[j] = (uint32_t)c; c >>= 32;
-  }
-}
-
 /* The pipe's top-digit position for the wave (its longest scalar has nbits
    bits): P = nbits - 3, within [124, 252]. */
 __device__ __forceinline__ int wave_top_pos( int nbits ) {
 #pragma unroll
   for( int o=32; o>=1; o>>=1 ) nbits = max( nbits, __shfl_xor( nbits, o ) );
-  return min( 4*(FD_NDIG_MAX-2) + 4, max( 124, nbits - 3 ) );
+  return recode_p_top( nbits );
 }
 
 /* recode_p_lds: ybias_p's digits into nw LDS byte rows (biased by 8, negated
@@ -410,22 +390,16 @@ __device__ __forceinline__ int wave_top_pos( int nbits ) {
 __device__ __forceinline__ void recode_p_lds( uint8_t * row, uint32_t const x[ 8 ], int neg, int P, uint64_t stride ) {
   uint32_t y[ 8 ];
   ybias_p( y, x, P );
-  int nw = ((P + 3) >> 2) + 1, wn = P - 4*(nw - 2);
+  int nw = ((P + 3) >> 2) + 1;
 #pragma unroll
-  for( int i=0; i<FD_NDIG_MAX; i++ ) {
-    if( i < nw ) {
-      uint32_t db;
-      if( i == nw-1 ) {                              /* the top digit: bit P = 4 (i-1) + wn */
-        int j = i - 1 < 0 ? 0 : i - 1;
-        uint64_t two = (uint64_t)y[ j >> 3 ] | ((j >> 3) < 7 ? (uint64_t)y[ (j >> 3) + 1 ] << 32 : 0ull);
-        db = ((uint32_t)(two >> (4*(j & 7) + wn)) & 15u) + 8u;
-      } else {
-        db = (y[ i >> 3 ] >> (4*(i & 7))) & 15u;
-        if( i == nw-2 ) db = (db & ((1u << wn) - 1u)) + 8u - (1u << (wn - 1));
-      }
+  for( int i=0; i<FD_NDIG_MAX-1; i++ ) {
+    if( i < nw-1 ) {
+      uint32_t db = recode_p_low( y, i, P );
       row[ (uint64_t)i*stride ] = (uint8_t)(neg ? 16u - db : db);
     }
   }
+  uint32_t db = recode_p_hi( y, P );
+  row[ (uint64_t)(nw-1)*stride ] = (uint8_t)(neg ? 16u - db : db);
 }
 
 /* k = SHA-512(R||A||M) mod l (:203-206), the lattice vector (u, v, sign

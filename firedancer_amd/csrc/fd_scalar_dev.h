@@ -151,4 +151,43 @@ FD_SC_FN int comb_digit( uint32_t const y[ 8 ], int k ) {
   return comb_digit_w( y[q], q < 7 ? y[q+1] : 0u, k );
 }
 
+
+/* The verify kernels' recoding of the lattice scalars u, v (x < 2^(P+3)): the
+   top digit at bit P (P = nbits - 3 of the wave's longest scalar, at least
+   124: recode_p_top), so the Straus chain takes P doublings rather than the
+   next multiple of four; windows 0 .. m-2 are 4-bit (bias 8 each), window
+   m-1 = nw-2 is wn = P - 4 (m-1) bits (bias 2^(wn-1)), the top digit is
+   y >> P; m = ceil(P / 4), nw = m + 1.  x < 2^(P+3) keeps the top digit <= 8
+   (y < 8.77 2^P).  Pinned on the CPU through this code by
+   tests/test_field_bounds.py::test_pipe_recoding. */
+FD_SC_FN int recode_p_top( int nbits ) {
+  int P = nbits - 3;
+  P = P < 124 ? 124 : P;
+  return P > 252 ? 252 : P;          /* 4 (FD_NDIG_MAX - 2) + 4: 64 windows */
+}
+FD_SC_FN void ybias_p( uint32_t y[ 8 ], uint32_t const x[ 8 ], int P ) {
+  int m = (P + 3) >> 2, wn = P - 4*(m - 1), eb = 4*(m - 1) + wn - 1;
+  uint64_t c = 0;
+#pragma unroll
+  for( int j=0; j<8; j++ ) {
+    int nb = m - 1 - 8*j;                           /* 4-bit biased nibbles in word j */
+    uint32_t pat = nb >= 8 ? 0x88888888u : (nb <= 0 ? 0u : (0x88888888u & ((1u << (4*nb)) - 1u)));
+    uint32_t ex = (eb >> 5) == j ? (1u << (eb & 31)) : 0u;
+    c += (uint64_t)x[j] + pat + ex;
+    y[j] = (uint32_t)c; c >>= 32;
+  }
+}
+/* Digit i < nw-1 of a ybias_p scalar, biased: d_i + 8 in [0, 16]. */
+FD_SC_FN uint32_t recode_p_low( uint32_t const y[ 8 ], int i, int P ) {
+  int nw = ((P + 3) >> 2) + 1, wn = P - 4*(nw - 2);
+  uint32_t db = (y[ i >> 3 ] >> (4*(i & 7))) & 15u;
+  return i == nw-2 ? (db & ((1u << wn) - 1u)) + 8u - (1u << (wn - 1)) : db;
+}
+/* The top digit (i = nw-1, at bit P), biased. */
+FD_SC_FN uint32_t recode_p_hi( uint32_t const y[ 8 ], int P ) {
+  int q = P >> 5;
+  uint64_t two = (uint64_t)y[ q ] | (q < 7 ? (uint64_t)y[ q + 1 ] << 32 : 0ull);
+  return ((uint32_t)(two >> (P & 31)) & 15u) + 8u;
+}
+
 #endif /* FD_SCALAR_DEV_H */

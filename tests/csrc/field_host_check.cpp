@@ -24,6 +24,13 @@ void t_sc_reduce( uint32_t * r, uint32_t const * x ) { sc_reduce512( r, x ); }
 int  t_sc_lt_l( uint32_t const * s ) { return sc_lt_l( s ); }
 void t_recode4( uint8_t * o, uint32_t const * s ) { sc_recode_w4( o, s ); }
 void t_recode8( uint8_t * o, uint32_t const * s ) { sc_recode_w8( o, s ); }
+int  t_recode_p_top( int nbits ) { return recode_p_top( nbits ); }
+void t_recode_p( uint8_t * o, uint32_t const * x, int P ) {    /* ybias_p's digits, biased */
+  uint32_t y[ 8 ]; ybias_p( y, x, P );
+  int nw = ((P + 3) >> 2) + 1;
+  for( int i=0; i<nw-1; i++ ) o[i] = (uint8_t)recode_p_low( y, i, P );
+  o[nw-1] = (uint8_t)recode_p_hi( y, P );
+}
 void t_sha_block( uint64_t * h, uint64_t * w ) { sha512_compress( h, w ); }
 void t_comb_digits( int * d, uint32_t const * w ) {
   uint32_t y[ 8 ]; comb_bias( y, w );

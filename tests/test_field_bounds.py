@@ -328,42 +328,38 @@ def test_dbl_host_projective(lib):
         assert all(in_R(o[10 * k:10 * k + 10]) for k in range(4))
 
 
-def test_pipe_recoding():
-    """The pipe kernel's scalar recoding (fd_ed25519_gpu_kern.hip ybias_p /
-    ydig_p / wave_top_pos, restated): for the wave's top-digit position
-    P = clamp(nbits - 3, 124, 252) every scalar x < 2^nbits is the sum of its
-    signed digits -- windows 0..nw-3 4-bit in [-8, 8), window nw-2 wn bits
-    in [-2^(wn-1), 2^(wn-1)), the top digit in [0, 8] at bit P -- so the
-    chain's P doublings and the 9-entry tables (|d| <= 8) cover it."""
+def test_pipe_recoding(lib):
+    """The verify kernels' scalar recoding (fd_scalar_dev.h recode_p_top /
+    ybias_p / recode_p_low / recode_p_hi, compiled for the host; ydig_p in
+    fd_ed25519_gpu_kern.hip reads the same bits out of LDS): for the wave's
+    top-digit position P = clamp(nbits - 3, 124, 252) every scalar x < 2^nbits
+    is the sum of its signed digits -- windows 0..nw-3 4-bit in [-8, 8),
+    window nw-2 wn bits in [-2^(wn-1), 2^(wn-1)), the top digit in [0, 8] at
+    bit P -- so the chain's P doublings and the 9-entry tables (|d| <= 8)
+    cover it.  The same digits from a Python restatement."""
     rng = random.Random(77)
+    lib.t_recode_p_top.restype = ctypes.c_int
 
-    def top_pos(nbits):
-        return min(4 * (64 - 2) + 4, max(124, nbits - 3))
-
-    def digits(x, P):
+    def model(x, P):
         m = (P + 3) >> 2
         wn = P - 4 * (m - 1)
         nw = m + 1
-        bias = sum(8 << (4 * i) for i in range(m - 1)) + (1 << (4 * (m - 1) + wn - 1))
-        y = x + bias
-        assert y < 2**256
-        out = []
-        for i in range(nw):
-            if i == nw - 1:
-                d = (y >> P) & 15
-                assert y >> P == d                      # nothing above the top digit
-            else:
-                nib = (y >> (4 * i)) & 15
-                d = (nib & ((1 << wn) - 1)) - (1 << (wn - 1)) if i == nw - 2 else nib - 8
-            out.append(d)
-        pos = [4 * i for i in range(nw - 1)] + [P]
-        return out, pos, wn
+        y = x + sum(8 << (4 * i) for i in range(m - 1)) + (1 << (4 * (m - 1) + wn - 1))
+        assert y < 2**256 and y >> P <= 8                 # nothing above the top digit
+        d = [((y >> (4 * i)) & 15) - 8 for i in range(nw - 2)]
+        d.append(((y >> (4 * (nw - 2))) & ((1 << wn) - 1)) - (1 << (wn - 1)))
+        d.append(y >> P)
+        return d, [4 * i for i in range(nw - 1)] + [P], wn
 
     for nbits in list(range(1, 254)) + [128, 129, 130, 131, 132, 133, 134] * 20:
-        P = top_pos(nbits)
+        P = lib.t_recode_p_top(nbits)
+        assert P == min(252, max(124, nbits - 3))
         for x in [(1 << nbits) - 1, 1 << (nbits - 1), rng.randrange(1 << nbits), 0]:
-            d, pos, wn = digits(x, P)
+            d, pos, wn = model(x, P)
             assert sum(di << p for di, p in zip(d, pos)) == x
             assert 0 <= d[-1] <= 8
             assert all(-8 <= di < 8 for di in d[:-2]) and -(1 << (wn - 1)) <= d[-2] < (1 << (wn - 1))
             assert pos[-1] == P and pos[-1] - pos[-2] == wn     # the chain's doublings: P in all
+            o = (ctypes.c_uint8 * 64)()
+            lib.t_recode_p(o, arr([(x >> (32 * j)) & 0xffffffff for j in range(8)]), P)
+            assert [o[i] - 8 for i in range(len(d))] == d
