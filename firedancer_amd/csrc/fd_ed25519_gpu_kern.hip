@@ -1058,8 +1058,13 @@ __device__ __forceinline__ uint32_t pipe_len_order( uint32_t key, int w, int lan
    stride cap) into its LDS column block y[nwords][64]. */
 __device__ __forceinline__ void hand_to_lds( uint32_t * y, uint32_t const * hand, uint64_t cap, uint64_t gid, int lane,
                                              int w0, int nwords ) {
-#pragma unroll 1
-  for( int j=0; j<nwords; j++ ) y[ j*64 + lane ] = hand[ (uint64_t)(w0 + j)*cap + gid ];
+  /* all loads first, then the LDS stores: one memory round trip at the
+     wave's start instead of one per word (a rolled loop waited for each) */
+  uint32_t t[ 24 ];
+#pragma unroll
+  for( int j=0; j<24; j++ ) t[j] = j < nwords ? hand[ (uint64_t)(w0 + j)*cap + gid ] : 0u;
+#pragma unroll
+  for( int j=0; j<24; j++ ) if( j < nwords ) y[ j*64 + lane ] = t[j];
 }
 
 extern "C" __global__ void __launch_bounds__( 3 * FD_VERIFY_BLOCK, 1 )
@@ -1205,18 +1210,26 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       stA = (ok ? 1 : 0) | (sm ? 2 : 0);
       FE_FENCE();
     }
+    /* A's status as two wave ballots (SGPRs) and R's encoding addressed from
+       an opaque copy of gid: neither a status VGPR nor the hand-off address
+       stays live across R's decode (both were spilled at 168 VGPRs) */
+    uint64_t m_aok = __ballot( (stA & 1) != 0 ), m_asm = __ballot( (stA & 2) != 0 );
+    uint64_t gr = gid;
+    asm volatile( "" : "+v"(gr) );
     if( desc_ok && !bad_s ) {                         /* R = sig[0:32]: decode, small order, table */
       uint32_t enc[ 8 ];
 #pragma unroll
-      for( int j=0; j<8; j++ ) enc[j] = hand[ (uint64_t)(FD_PH_R + j)*cap + gid ];
+      for( int j=0; j<8; j++ ) enc[j] = hand[ (uint64_t)(FD_PH_R + j)*cap + gr ];
       ge_p3 Q;
       int ok = ge_decode( Q, enc, !args.ref_codes );
       int sm = ge_affine_small_order( Q );
       FE_FENCE();
-      if( ok && !sm && (stA & 1) && !(stA & 2) ) vtab_build( args.vtab, vcap, (2u*set + 1u)*cap + gid, Q );
+      bool aok = (m_aok >> lane) & 1u, asm_ = (m_asm >> lane) & 1u;
+      if( ok && !sm && aok && !asm_ ) vtab_build( args.vtab, vcap, (2u*set + 1u)*cap + gid, Q );
       stR = (ok ? 1 : 0) | (sm ? 2 : 0);
       FE_FENCE();
     }
+    stA = (int)((m_aok >> lane) & 1u) | (int)(((m_asm >> lane) & 1u) << 1);
     code = verify_precode( args, desc_ok, bad_s, stA, stR );
     if( valid ) a.code_b[ gid ] = (int8_t)code;
   } else {
