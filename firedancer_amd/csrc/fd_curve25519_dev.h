@@ -170,7 +170,16 @@ FD_GE_FN void fe_invert( fe & out, fe const & z ) {
    (not reduced), u = y^2-1, v = dy^2+1, x = uv^3 (uv^7)^((p-5)/8); fail if
    neither vx^2 == u nor vx^2 == -u; x *= sqrt(-1) in the second case.
    avx512_rule: also fail on x == 0 with sign bit 1 (fd_r43x6_ge.c:139-140). */
-FD_GE_FN int ge_decode( ge_p3 & P, uint32_t const w[ 8 ], bool avx512_rule ) {
+FD_GE_FN int ge_decode_small( ge_p3 & P, uint32_t const w[ 8 ], bool avx512_rule, int * small );
+FD_GE_FN int ge_decode( ge_p3 & P, uint32_t const w[ 8 ], bool avx512_rule ) { int sm; return ge_decode_small( P, w, avx512_rule, &sm ); }
+
+/* ge_decode plus the order <= 8 test of the decoded point (*small;
+   meaningful when the decode succeeds): x == 0 from the bytes of x the
+   decode computes anyway, and y's canonical value in {0, y0, y1} read off
+   the encoding: y is w with bit 255 cleared, so its canonical value is 0, y0
+   or y1 iff that word string is 0, p, y0 or y1 (y0 + p and y1 + p are past
+   2^255).  Equals ge_affine_small_order on the decoded point. */
+FD_GE_FN int ge_decode_small( ge_p3 & P, uint32_t const w[ 8 ], bool avx512_rule, int * small ) {
   fe one, d, y, y2, u, v, v2, v3, v4, uv3, uv7, t, x, x2, vxx, chk;
   fe_set1( one ); fe_const_d( d );
   int sign = (int)(w[7] >> 31);
@@ -214,6 +223,18 @@ FD_GE_FN int ge_decode( ge_p3 & P, uint32_t const w[ 8 ], bool avx512_rule ) {
   P.X = x; P.Y = y; fe_set1( P.Z );
   fe_mul( P.T, x, y );
   FE_FENCE();
+  {
+    uint32_t const y0[ 8 ] = { 0x8f95e826u,0xb027b2c2u,0x89f4c345u,0xf098eff2u,0x05acdfd5u,0x3933c6d3u,0x880238b1u,0x05fc536du };
+    uint32_t const y1[ 8 ] = { 0x706a17c7u,0x4fd84d3du,0x760b3cbau,0x0f67100du,0xfa53202au,0xc6cc392cu,0x77fdc74eu,0x7a03ac92u };
+    uint32_t yo = 0u, ep = 0u, e0 = 0u, e1 = 0u;
+#pragma unroll
+    for( int i=0; i<8; i++ ) {
+      uint32_t wi = i == 7 ? (w[7] & 0x7fffffffu) : w[i];
+      uint32_t pi = i == 0 ? 0xffffffedu : (i == 7 ? 0x7fffffffu : 0xffffffffu);
+      yo |= wi; ep |= wi ^ pi; e0 |= wi ^ y0[i]; e1 |= wi ^ y1[i];
+    }
+    *small = x_zero | (yo == 0u) | (ep == 0u) | (e0 == 0u) | (e1 == 0u);
+  }
   return ok;
 }
 

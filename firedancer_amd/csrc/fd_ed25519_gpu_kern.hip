@@ -816,8 +816,8 @@ fd_ed25519_verify_kernel( verify_args args ) {
 #pragma unroll
       for( int j=0; j<8; j++ ) enc[j] = encs[ (8*q + j)*64 + lane ];
       ge_p3 Q;
-      int ok = ge_decode( Q, enc, !args.ref_codes );
-      int sm = ge_affine_small_order( Q );
+      int sm;
+      int ok = ge_decode_small( Q, enc, !args.ref_codes, &sm );
       FE_FENCE();
       if( ok && !sm ) vtab_build( args.vtab, cap, (uint64_t)q*cap/2u + gid, Q );
       int s = (ok ? 1 : 0) | (sm ? 2 : 0);
@@ -926,8 +926,8 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
 #pragma unroll
     for( int j=0; j<8; j++ ) enc[j] = role ? sig[j] : pub[j];
     ge_p3 Q;
-    int ok = ge_decode( Q, enc, !args.ref_codes );
-    int sm = ge_affine_small_order( Q );
+    int sm;
+    int ok = ge_decode_small( Q, enc, !args.ref_codes, &sm );
     FE_FENCE();
     if( ok && !sm ) vtab_build( args.vtab, cap, (uint64_t)role*cap/2u + gid, Q );
     stq = (ok ? 1 : 0) | (sm ? 2 : 0);
@@ -1203,8 +1203,8 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #pragma unroll
       for( int j=0; j<8; j++ ) enc[j] = hand[ (uint64_t)(FD_PH_A + j)*cap + gid ];
       ge_p3 Q;
-      int ok = ge_decode( Q, enc, !args.ref_codes );
-      int sm = ge_affine_small_order( Q );
+      int sm;
+      int ok = ge_decode_small( Q, enc, !args.ref_codes, &sm );
       FE_FENCE();
       if( ok && !sm ) vtab_build( args.vtab, vcap, (2u*set)*cap + gid, Q );
       stA = (ok ? 1 : 0) | (sm ? 2 : 0);
@@ -1221,8 +1221,8 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #pragma unroll
       for( int j=0; j<8; j++ ) enc[j] = hand[ (uint64_t)(FD_PH_R + j)*cap + gr ];
       ge_p3 Q;
-      int ok = ge_decode( Q, enc, !args.ref_codes );
-      int sm = ge_affine_small_order( Q );
+      int sm;
+      int ok = ge_decode_small( Q, enc, !args.ref_codes, &sm );
       FE_FENCE();
       bool aok = (m_aok >> lane) & 1u, asm_ = (m_asm >> lane) & 1u;
       if( ok && !sm && aok && !asm_ ) vtab_build( args.vtab, vcap, (2u*set + 1u)*cap + gid, Q );
@@ -1434,9 +1434,9 @@ fd_ed25519_ktab_build_kernel( uint32_t * ktab, uint32_t * kmeta, uint32_t const 
   for( int j=0; j<8; j++ ) pub[j] = pubs[ i*8u + (uint64_t)j ];
   uint64_t slot = slots[ i ];
   ge_p3 A, A2;
-  int ok_ref = ge_decode( A, pub, false );
-  int ok_avx = ge_decode( A2, pub, true );
-  int sm = ge_affine_small_order( A );
+  int sm, sm2;
+  int ok_ref = ge_decode_small( A, pub, false, &sm );
+  int ok_avx = ge_decode_small( A2, pub, true, &sm2 );
   uint32_t * m = kmeta + slot * FD_KMETA_WORDS;
 #pragma unroll
   for( int j=0; j<8; j++ ) m[j] = pub[j];
@@ -1600,8 +1600,8 @@ fd_ed25519_verify_cached_kernel( verify_args args ) {
   if( live ) hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );   /* :203-206 */
   FE_FENCE();
   ge_p3 R;
-  int okR = ge_decode( R, sig, !args.ref_codes );                        /* :162 (R after A) */
-  int smR = ge_affine_small_order( R );
+  int smR;
+  int okR = ge_decode_small( R, sig, !args.ref_codes, &smR );             /* :162 (R after A) */
   bool okA = (st & (args.ref_codes ? FD_KST_OK_REF : FD_KST_OK_AVX)) != 0u;
   int code;
   if     ( !desc_ok            ) code = FD_ED25519_GPU_CODE_BAD_DESC;

@@ -56,6 +56,14 @@ void t_dbl( uint32_t * r, uint32_t const * p ) {
   ge_dbl( o, a, true );
   for( int i=0;i<10;i++ ){ r[i]=o.X.v[i]; r[10+i]=o.Y.v[i]; r[20+i]=o.Z.v[i]; r[30+i]=o.T.v[i]; }
 }
+int t_is_zero( uint32_t const * f ) { fe a; for( int i=0;i<10;i++ ) a.v[i]=f[i]; return fe_is_zero( a ); }
+/* decode with the kernels' small-order flag, and the flag of the affine
+   test on the decoded point (bytes of X and Y), for comparison */
+int t_decode_small( uint32_t const * w, int avx512_rule, int * small, int * small_affine ) {
+  ge_p3 P; int ok = ge_decode_small( P, w, avx512_rule != 0, small );
+  *small_affine = ge_affine_small_order( P );
+  return ok;
+}
 }
 extern "C" {
 /* The host build of fd_fe_test_kernel's operations (fd_ed25519_gpu_kern.hip):

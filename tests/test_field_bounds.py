@@ -363,3 +363,54 @@ def test_pipe_recoding(lib):
             o = (ctypes.c_uint8 * 64)()
             lib.t_recode_p(o, arr([(x >> (32 * j)) & 0xffffffff for j in range(8)]), P)
             assert [o[i] - 8 for i in range(len(d))] == d
+
+
+def test_is_zero_r(lib):
+    """fe_is_zero (one carry pass, then 0 or p) on R-form limbs: equals
+    value % p == 0 at the R bounds, for 0 and p in many limb forms and for
+    values just past 2^255."""
+    rng = random.Random(91)
+    lib.t_is_zero.restype = ctypes.c_int
+    pl = [2**26 - 19] + [(2**25 - 1) if i & 1 else (2**26 - 1) for i in range(1, 10)]
+
+    def limbs(x):            # a random R-form representation of x (x < 2^255 + small)
+        h = []
+        for i in range(10):
+            w = 25 if i & 1 else 26
+            h.append(x & ((1 << w) - 1)); x >>= w
+        h[9] += x << 25 if x else 0
+        for _ in range(rng.randrange(4)):                  # move carries down within R bounds
+            i = rng.randrange(9)
+            w = 25 if i & 1 else 26
+            if h[i + 1] > 0 and h[i] + (1 << w) <= (R_O if i & 1 else R_E):
+                h[i + 1] -= 1; h[i] += 1 << w
+        return h
+    cases = [[0] * 10, pl, [R_E, R_O] * 5, [x + (1 << 11) if i % 2 == 0 else x for i, x in enumerate(pl)]]
+    for _ in range(3000):
+        cases.append(limbs(rng.randrange(P)))
+        cases.append(limbs(rng.choice([0, P, rng.randrange(2**255, 2**255 + 2**200)])))
+        cases.append([rng.randrange(R_E + 1) if i % 2 == 0 else rng.randrange(R_O + 1) for i in range(10)])
+    for h in cases:
+        assert all(v < 2**31 for v in h)
+        assert lib.t_is_zero(arr(h)) == (val(h) % P == 0), h
+
+
+def test_decode_small_order_flag(lib):
+    """ge_decode_small's order <= 8 flag (x == 0 from the decode's own bytes,
+    y in {0, p, y0, y1} read off the encoding) equals the affine test on
+    the decoded point, for the small-order encodings, y = p + v, random
+    encodings and both sign bits, in both decode rules."""
+    rng = random.Random(92)
+    y0 = 0x05fc536d880238b13933c6d305acdfd5f098eff289f4c345b027b2c28f95e826
+    y1 = 0x7a03ac9277fdc74ec6cc392cfa53202a0f67100d760b3cba4fd84d3d706a17c7
+    ys = [0, 1, P - 1, P, y0, y1, P - y0, P - y1, 2**255 - 1] + [P + v for v in range(19)]
+    ys += [rng.randrange(2**255) for _ in range(400)]
+    sm, sma = ctypes.c_int(), ctypes.c_int()
+    for y in ys:
+        for sign in (0, 1):
+            e = y | (sign << 255)
+            w = arr([(e >> (32 * j)) & 0xffffffff for j in range(8)])
+            for rule in (0, 1):
+                ok = lib.t_decode_small(w, rule, ctypes.byref(sm), ctypes.byref(sma))
+                if ok:
+                    assert sm.value == sma.value, (hex(y), sign, rule)
