@@ -495,7 +495,11 @@ def main():
              else "fd_ed25519_verify_kernel")
     if rank == 0:
         peak = valu_peak()
-        achieved = W_MAC * n / (launch_ms * 1e-3)
+        # priced on the step (the wall-timed ms_per_step, launch gap included,
+        # per GPU), as `value` is; the event-bracketed kernel time gives
+        # kernel_frac beside it
+        achieved = W_MAC * value / world
+        kernel_achieved = W_MAC * n / (launch_ms * 1e-3)
         build = fa.build_id()
         traffic, traffic_src = pmc_traffic(n, kname, build.get("code")) if args.config == 2 else (None, "config 2 only")
         line = {
@@ -516,7 +520,9 @@ def main():
             "roofline": {"bound": "valu-int32", "achieved": achieved / 1e12, "peak": peak / 1e12,
                          "unit": "T MAC/s (32x32->64 multiply-adds, W=%.4g per verify)" % W_MAC,
                          "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel_ms": launch_ms},
+                         "priced_on": "ms_per_step (wall clock per step, per GPU: W x value / n_gpus)",
+                         "kernel_ms": launch_ms, "kernel_frac": kernel_achieved / peak,
+                         "kernel_frac_note": "the same W priced on the mean event-bracketed launch (no inter-launch gap)"},
             "cpu_baseline": None,
             "warmup_detail": {"prime_steps": prime, "prime_ms": args.prime_ms, "warmup_steps": args.warmup,
                               "untimed_steps_total": prime + args.warmup,
@@ -539,7 +545,7 @@ def main():
         # from the PMC-measured bytes per launch of this build's committed profile.
         t = traffic
         if t:
-            gbs = t / (launch_ms * 1e-3) / 1e9
+            gbs = t / (dt_max / args.steps) / 1e9
             line["roofline_hbm"] = {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
                                     "frac": gbs / 8000.0, "traffic": t}
         # The same work priced at the clock the chip held in this build's profiled

@@ -16,6 +16,7 @@ from .ed25519 import (  # noqa: F401
     CODES_AVX512, CODES_REF, DESC_DTYPE, PRECOMPILE_DTYPE, SPAN_DTYPE, SHA_MSG_DTYPE, Ed25519Gpu, GpuError, lib_path, load_lib, pack_batch,
     strerror, txn_reduce, ctab_stats, build_id, gossip_walk, gossip_walk_crds, GOSSIP_CORRUPT, GOSSIP_UNSIGNED, GOSSIP_NOT_MINE, GOSSIP_CRDS,
     QUEUE_DEPTH,
+    STAGE_DEPTH,
     GOSSIP_NO_VALUES,
     shred_walk, sha256, SHRED_PARSE, SHRED_ZERO_SIG, SHRED_COUNTS, SHRED_INDEX, SHRED_DEPTH, SHRED_PROOF,
 )

@@ -43,6 +43,12 @@ FD_FN void fe_const_sqrtm1( fe & r ) {
   r.v[5]=0x1fbd7a7u; r.v[6]=0x2804c9eu; r.v[7]=0x1e16569u; r.v[8]=0x004fc1du; r.v[9]=0x0ae0c92u;
 }
 
+/* 1/d */
+FD_FN void fe_const_invd( fe & r ) {
+  r.v[0]=0x1c9f843u; r.v[1]=0x03c9db3u; r.v[2]=0x285c4bcu; r.v[3]=0x0c213cau; r.v[4]=0x02d775au;
+  r.v[5]=0x1b9cf66u; r.v[6]=0x3108a66u; r.v[7]=0x1c86562u; r.v[8]=0x1214d5cu; r.v[9]=0x10241fbu;
+}
+
 FD_FN void ge_identity( ge_p3 & p ) { fe_set0( p.X ); fe_set1( p.Y ); fe_set1( p.Z ); fe_set0( p.T ); }
 
 /* r = 2p (dbl-2008-hwcd, a=-1).  p.X,Y,Z in R.  T computed iff want_t.
@@ -152,6 +158,26 @@ FD_FN void ge_to_cached( ge_cached & c, ge_p3 const & p ) {
   fe_mul( c.T2d, p.T, d2 );
   FE_FENCE();
   fe_add( c.Z2, p.Z, p.Z );
+}
+
+/* The extended point of a cached entry (Y+X, Y-X, 2dT, 2Z), scaled by 2:
+   (Y+X - (Y-X), Y+X + Y-X, 2Z, 2dT / d) = (2X, 2Y, 2Z, 2T), the same
+   projective point -- what identity + entry gives, for ~1/4 of an addition
+   (the Straus chain's first window).  Y+X and Y-X may be M (the cached
+   form's bound), so the difference takes a 4p bias; 2dT may be M (a
+   negated entry); every output is carried to R. */
+FD_FN void ge_from_cached( ge_p3 & r, ge_cached const & c ) {
+  fe t;
+  t.v[0] = c.YpX.v[0] + FE_4P0 - c.YmX.v[0];
+#pragma unroll
+  for( int i=1; i<10; i++ ) t.v[i] = c.YpX.v[i] + ((i&1) ? FE_4PO : FE_4PE) - c.YmX.v[i];
+  fe_carry( r.X, t );
+  fe_add( t, c.YpX, c.YmX );
+  fe_carry( r.Y, t );
+  fe_carry( r.Z, c.Z2 );
+  fe invd; fe_const_invd( invd );
+  fe_mul( r.T, c.T2d, invd );
+  FE_FENCE();
 }
 
 /* 1/z = z^(p-2) = (z^(2^252-3))^8 * z^3 */

@@ -118,8 +118,11 @@ struct pipe_args {
   int8_t const *            code_c;
   uint64_t                  n_c;        /* 0: no batch in phase C */
   int8_t *                  out_c;      /* the codes of batch j-2 */
-  uint32_t *                err;        /* host-mapped error word: set to 1 when a phase-A wait expires */
+  uint32_t *                err;        /* host-mapped error ring (FD_PIPE_ERR_RING words): a phase-A wait that
+                                           expires stores seq + 1 at err[seq % FD_PIPE_ERR_RING] */
+  uint64_t                  seq;        /* the pipe counter of the batch in phase A (its codes are the ones at risk) */
 };
+#define FD_PIPE_ERR_RING  64
 
 struct kpart_args {
   uint8_t const *           arena;
@@ -196,6 +199,7 @@ struct shred_root_args {
 #define FD_KERN_PIPE     "fd_ed25519_verify_pipe_kernel"
 #define FD_KERN_SHA256   "fd_sha256_batch_kernel"
 #define FD_KERN_SROOT    "fd_shred_root_kernel"
+#define FD_KERN_IDFILL   "fd_vtab_id_fill"
 /* Waves per workgroup of the single-lane kernel: one, so the dispatcher
    refills each SIMD's wave slot as soon as that wave ends (four-wave
    workgroups held a slot until the workgroup's longest wave ended). */

@@ -25,6 +25,25 @@
 #include "fd_scalar_dev.h"
 #include "fd_lattice_dev.h"
 
+/* Round-4 instruction cuts, each a build switch for same-process A/Bs
+   (tools/ab_b2b.py; -DFD_OPT_X=0 builds the previous form):
+     FIRSTWIN  the chain's first window takes its entry as the point
+               (ge_from_cached) instead of adding it to the identity;
+     COMBCHK   the last comb addition folded into the final compare
+               (comb_lds_eq);
+     IDROW     row 0 of every variable-base table pre-filled with the
+               identity (fd_vtab_id_fill at allocation) instead of a shared
+               record selected per fetch. */
+#ifndef FD_OPT_FIRSTWIN
+#define FD_OPT_FIRSTWIN 1
+#endif
+#ifndef FD_OPT_COMBCHK
+#define FD_OPT_COMBCHK 1
+#endif
+#ifndef FD_OPT_IDROW
+#define FD_OPT_IDROW 1
+#endif
+
 /* Diagnostic build only (-DFD_PHASE_STAMPS, tools/Makefile): s_memtime at
    phase boundaries, per-wave deltas summed into args.stamps.  The product
    build compiles none of it. */
@@ -193,10 +212,34 @@ __device__ __forceinline__ void vtab_ptrs( uint32_t const * vtab, uint64_t cap, 
   uint64_t idx = (uint64_t)e * cap + t;
   *m  = (uint4 const *)(vtab + idx * 32u);
   *tl = (uint4 const *)(vtab + (uint64_t)FD_VTAB_N * cap * 32u + idx * 8u);
+#if !FD_OPT_IDROW
   if( !e ) {   /* the identity: one shared record after both regions (written by the host) */
     uint32_t const * id = vtab + (uint64_t)FD_VTAB_N * cap * 40u;
     *m = (uint4 const *)id; *tl = (uint4 const *)(id + 32);
   }
+#endif
+}
+
+/* Row 0 of every table = the identity in cached form (Y+X = 1, Y-X = 1,
+   2dT = 0, 2Z = 2; FD_VW layout): written once when the table scratch is
+   allocated (no kernel ever stores row 0), so a fetch of digit 0 needs no
+   select of a shared record.  One thread per table. */
+extern "C" __global__ void __launch_bounds__( 256 ) fd_vtab_id_fill( uint32_t * vtab, uint64_t cap ) {
+  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if( t >= cap ) return;
+  uint4 * m  = (uint4 *)(vtab + t * 32u);
+  uint4 * tl = (uint4 *)(vtab + (uint64_t)FD_VTAB_N * cap * 32u + t * 8u);
+#pragma unroll
+  for( int j=0; j<8; j++ ) {
+    uint32_t w[ 4 ];
+#pragma unroll
+    for( int i=0; i<4; i++ ) {
+      int k = 4*j + i;
+      w[i] = (k == FD_VW( 0, 0 ) || k == FD_VW( 1, 0 )) ? 1u : (k == FD_VW( 3, 0 ) ? 2u : 0u);
+    }
+    m[j] = make_uint4( w[0], w[1], w[2], w[3] );
+  }
+  tl[0] = make_uint4( 0u, 0u, 0u, 0u ); tl[1] = make_uint4( 0u, 0u, 0u, 0u );
 }
 
 /* Entry |d| of a biased digit db = d + 8 (db <= 16 by construction; clamped
@@ -654,29 +697,54 @@ __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t co
                                            int nw, int hi, int lo, int wn ) {
   uint32_t dba = ydig_p( yu, lane, hi-1, nw, wn, uneg );
   vtab_fetch_lds( buf, vtab, cap, ta, dba );
+  uint32_t dbr = 0u;
+  bool skip_a = false;
+#if FD_OPT_FIRSTWIN
+  if( hi == nw ) {
+    /* the chain's first window (every caller starts a chain at hi = nw
+       from the identity): A's entry becomes the point itself
+       (ge_from_cached, ~1/4 of an addition), outside the loop so the loop
+       body's registers do not grow */
+    ge_cached q;
+    dma_wait();
+    uint32_t w[ 40 ];
+    lds_entry_words<10>( w, buf, lane, dba < 8u );
+    dbr = ydig_p( yv, lane, hi-1, nw, wn, false );
+    FE_FENCE();
+    vtab_fetch_lds( buf, vtab, cap, tr, dbr );
+    lds_entry_finish( q, w, dba < 8u );
+    FE_FENCE();
+    ge_from_cached( acc, q );
+    FE_FENCE();
+    skip_a = true;
+  }
+#endif
 #pragma unroll 1
   for( int i=hi-1; i>=lo; i-- ) {
-    if( i < nw-1 ) {
-      int nd = i == nw-2 ? wn : 4;                  /* window nw-2 is wn bits wide (ybias_p) */
+    if( !skip_a ) {
+      if( i < nw-1 ) {
+        int nd = i == nw-2 ? wn : 4;                /* window nw-2 is wn bits wide (ybias_p) */
 #pragma unroll 1
-      for( int j=1; j<nd; j++ ) { ge_dbl( acc, acc, false ); FE_FENCE(); }
-      ge_dbl( acc, acc, true );
+        for( int j=1; j<nd; j++ ) { ge_dbl( acc, acc, false ); FE_FENCE(); }
+        ge_dbl( acc, acc, true );
+        FE_FENCE();
+      }
+      ge_cached q;
+      {
+        dma_wait();
+        uint32_t w[ 40 ];
+        lds_entry_words<10>( w, buf, lane, dba < 8u );
+        dbr = ydig_p( yv, lane, i, nw, wn, false );
+        FE_FENCE();
+        vtab_fetch_lds( buf, vtab, cap, tr, dbr );   /* LDS reads issued before the DMA see the old bytes */
+        lds_entry_finish( q, w, dba < 8u );
+      }
+      FE_FENCE();
+      ge_add_cached( acc, acc, q, true );
       FE_FENCE();
     }
+    skip_a = false;
     ge_cached q;
-    uint32_t dbr;
-    {
-      dma_wait();
-      uint32_t w[ 40 ];
-      lds_entry_words<10>( w, buf, lane, dba < 8u );
-      dbr = ydig_p( yv, lane, i, nw, wn, false );
-      FE_FENCE();
-      vtab_fetch_lds( buf, vtab, cap, tr, dbr );     /* LDS reads issued before the DMA see the old bytes */
-      lds_entry_finish( q, w, dba < 8u );
-    }
-    FE_FENCE();
-    ge_add_cached( acc, acc, q, true );
-    FE_FENCE();
     {
       dma_wait();
       uint32_t w[ 40 ];
@@ -720,6 +788,60 @@ __device__ __forceinline__ void comb_lds( ge_p3 & acc, uint4 * buf, uint32_t con
     FE_FENCE();
   }
 #undef FD_WDIG
+}
+
+/* acc + [w]B == O, the comb additions of comb_lds but the last: Q = acc + C
+   with C = [d_10] B_10 is O iff acc = -C = (-x_C, y_C), i.e. (affine C,
+   projective acc, Z != 0 on the curve) 2X + (Y+X - (Y-X))_C Z = 0 and
+   2Y - (Y+X + Y-X)_C Z = 0: two products and the two zero tests instead
+   of the last mixed addition (7 products), the previous one's T and the
+   projective compare.  C's sign flips x_C only, so it is applied to the
+   first product.  Comb entries are R (ctab_init: carried sums). */
+__device__ __forceinline__ int comb_lds_eq( ge_p3 & acc, uint4 * buf, uint32_t const * yw, int lane, uint32_t const * ctab ) {
+#define FD_WDIG( k ) comb_digit_w( yw[ ((23*(k)) >> 5)*64 + lane ], ((23*(k)) >> 5) < 7 ? yw[ (((23*(k)) >> 5) + 1)*64 + lane ] : 0u, (k) )
+  int d = FD_WDIG( 0 );
+  ctab_fetch_lds( buf, ctab, 0, d );
+#pragma unroll 1
+  for( int k=0; k<FD_CTAB_POS-1; k++ ) {
+    ge_precomp bp;
+    {
+      dma_wait();
+      uint32_t w[ 32 ];
+      lds_words<8>( w, buf, lane );
+      int dn = FD_WDIG( k + 1 );
+      FE_FENCE();
+      ctab_fetch_lds( buf, ctab, k + 1, dn );
+      ctab_finish( bp, w, d );
+      d = dn;
+    }
+    FE_FENCE();
+    ge_madd( acc, acc, bp, k + 2 < FD_CTAB_POS );
+    FE_FENCE();
+  }
+#undef FD_WDIG
+  dma_wait();
+  fe yp, ym, t1, t2, e;
+  {
+    uint32_t w[ 32 ];
+    lds_words<8>( w, buf, lane );
+#pragma unroll
+    for( int j=0; j<10; j++ ) { yp.v[j] = w[j]; ym.v[j] = w[10+j]; }
+  }
+  fe_sub( e, yp, ym );                  /* M: 2 x_C of the unsigned entry */
+  fe_mul( t1, e, acc.Z );
+  FE_FENCE();
+  fe_add( e, yp, ym );                  /* M: 2 y_C */
+  fe_mul( t2, e, acc.Z );
+  FE_FENCE();
+  fe_cneg( t1, t1, d < 0 );
+  fe_lshl1_add( e, acc.X, t1 );         /* 2X + 2 x_C Z */
+  fe_carry( e, e );
+  int ex = fe_is_zero( e );
+  fe_add( yp, acc.Y, acc.Y );
+  fe_sub( e, yp, t2 );                  /* 2Y - 2 y_C Z */
+  fe_carry( e, e );
+  int ey = fe_is_zero( e );
+  return ex & ey;
 }
 
 /* One signature per lane:
@@ -836,13 +958,18 @@ fd_ed25519_verify_kernel( verify_args args ) {
     int nw = ((P + 3) >> 2) + 1, wn = P - 4*(nw - 2);  /* ybias_p's windows */
     ge_p3 acc; ge_identity( acc );
     chain_seg( acc, s_buf[ wv ], y, y + 8*64, lane, un != 0, args.vtab, cap, gid, cap/2u + gid, nw, nw, 0, wn );
+#if FD_OPT_COMBCHK
+    int eq = comb_lds_eq( acc, s_buf[ wv ], y + 16*64, lane, args.ctab );
+    STAMP( 5 );
+#else
     comb_lds( acc, s_buf[ wv ], y + 16*64, lane, args.ctab );
     STAMP( 5 );
     fe dl;
     int ex = fe_is_zero( acc.X );
     fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
-    int ey = fe_is_zero( dl );
-    code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+    int eq = ex & fe_is_zero( dl );
+#endif
+    code = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
   }
   args.out[ di ] = (int8_t)code;
 #ifdef FD_PHASE_STAMPS
@@ -1002,14 +1129,16 @@ __device__ __forceinline__ uint32_t len_bucket( fd_ed25519_desc_t const & d ) {
    Returns the descriptor index (within the workgroup) slot t = w*64 + lane
    takes.  The four waves wait for each other on LDS counters zeroed by the
    workgroup's barrier at kernel start (bounded waits: all four are resident
-   in the workgroup, so they arrive). */
+   in the workgroup, so they arrive).  An expired wait stores errv (the
+   batch's pipe counter + 1) into *err, the batch's word of the host-mapped
+   error ring. */
 #ifdef FD_DIAG_LSORT_TIMEOUT
 #define FD_LSORT_SPIN 0u            /* diagnostic build: every wait that is not already met expires */
 #else
 #define FD_LSORT_SPIN (1u << 20)
 #endif
 __device__ __forceinline__ uint32_t pipe_len_order( uint32_t key, int w, int lane, uint32_t * wh, uint32_t * perm,
-                                                    uint32_t * flag, uint32_t * err ) {
+                                                    uint32_t * flag, uint32_t * err, uint32_t errv ) {
   uint64_t below = (1ull << lane) - 1ull;
   uint32_t mine = 0, rank = 0;
 #pragma unroll 1
@@ -1045,7 +1174,7 @@ __device__ __forceinline__ uint32_t pipe_len_order( uint32_t key, int w, int lan
     __builtin_amdgcn_s_sleep( 1 );
   late |= __hip_atomic_load( &flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u;
   __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "workgroup" );
-  if( late && lane == 0 && err ) __hip_atomic_store( err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+  if( late && lane == 0 && err ) __hip_atomic_store( err, errv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
   return perm[ w*64 + lane ] & (FD_VERIFY_BLOCK - 1u);   /* in the workgroup's range whatever happened */
 }
 
@@ -1113,7 +1242,8 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
     uint64_t b0 = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK, di = gid;   /* di: the descriptor this lane verifies */
     if( a.lsort && b0 + FD_VERIFY_BLOCK <= nn )                       /* full workgroups only: all four waves here */
       di = b0 + pipe_len_order( len_bucket( args.desc[ gid ] ), wv, lane, s_lo, s_lo + 4*FD_LEN_NB,
-                                s_lo + 4*FD_LEN_NB + FD_VERIFY_BLOCK, a.err );
+                                s_lo + 4*FD_LEN_NB + FD_VERIFY_BLOCK,
+                                a.err ? a.err + (a.seq % FD_PIPE_ERR_RING) : nullptr, (uint32_t)a.seq + 1u );
     if( (gid & ~(uint64_t)63) >= nn ) {
       if( gid < args.n ) a.st_a[ gid ] = 0u;             /* past a device-side count: no batch slot */
       return;
@@ -1265,13 +1395,18 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
         o[ (uint64_t)(20+j)*cap ] = acc.Z.v[j]; o[ (uint64_t)(30+j)*cap ] = acc.T.v[j];
       }
     } else {
+#if FD_OPT_COMBCHK
+      /* [w]B and Q == O (:225-228 on [v]D) folded into the last comb entry */
+      int eq = comb_lds_eq( acc, buf, y + 16*64, lane, args.ctab );
+#else
       comb_lds( acc, buf, y + 16*64, lane, args.ctab );
       /* Q == O  <=>  X == 0 and Y == Z (:225-228 on [v]D) */
       fe dl;
       int ex = fe_is_zero( acc.X );
       fe_sub( dl, acc.Y, acc.Z ); fe_carry( dl, dl );
-      int ey = fe_is_zero( dl );
-      code = (ex & ey) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+      int eq = ex & fe_is_zero( dl );
+#endif
+      code = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
     }
   }
   if( !phb && valid ) a.out_c[ hand[ (uint64_t)FD_PH_IDX*cap + gid ] ] = (int8_t)code;
@@ -1713,8 +1848,17 @@ fd_frag_scan_kernel( fparse_args a ) {
   uint32_t t = threadIdx.x;
   uint64_t per = (a.n + 1023u) / 1024u;
   uint64_t lo = (uint64_t)t * per, hi = min( a.n, lo + per );
+  /* the chunk's counts in rounds of 16 independent loads (a rolled loop
+     waited one memory round trip per count: 53 us for a 32K-frag batch,
+     profiles/r04/stage_trace) */
   uint32_t sum = 0u;
-  for( uint64_t i=lo; i<hi; i++ ) sum += a.cnt[ i ];
+  for( uint64_t i0=lo; i0<hi; i0+=16u ) {
+    uint32_t v[ 16 ];
+#pragma unroll
+    for( int j=0; j<16; j++ ) v[j] = i0 + (uint64_t)j < hi ? a.cnt[ i0 + (uint64_t)j ] : 0u;
+#pragma unroll
+    for( int j=0; j<16; j++ ) sum += v[j];
+  }
   part[ t ] = sum;
   __syncthreads();
   for( uint32_t o=1u; o<1024u; o<<=1 ) {
@@ -1724,7 +1868,13 @@ fd_frag_scan_kernel( fparse_args a ) {
     __syncthreads();
   }
   uint32_t run = part[ t ] - sum;                 /* exclusive */
-  for( uint64_t i=lo; i<hi; i++ ) { uint32_t c = a.cnt[ i ]; a.cnt[ i ] = run; run += c; }
+  for( uint64_t i0=lo; i0<hi; i0+=16u ) {
+    uint32_t v[ 16 ];
+#pragma unroll
+    for( int j=0; j<16; j++ ) v[j] = i0 + (uint64_t)j < hi ? a.cnt[ i0 + (uint64_t)j ] : 0u;
+#pragma unroll
+    for( int j=0; j<16; j++ ) if( i0 + (uint64_t)j < hi ) { a.cnt[ i0 + (uint64_t)j ] = run; run += v[j]; }
+  }
   if( t == 1023u ) *a.total = part[ 1023 ];
 }
 

@@ -7,10 +7,12 @@
    (so its bytes are one contiguous span for the copy to HBM) and holds at
    most max_batch frags.  With nothing outstanding any available frags go at
    once; with batches outstanding the next is submitted when at least
-   max_batch/2 frags wait -- so under load batches grow to max_batch and up
-   to FD_ED25519_GPU_QUEUE_DEPTH are in flight (the pipelined kernel runs one
-   phase of three of them per launch, two launches queued behind), and at low load latency stays at one batch: the stage finishes
-   a lone batch with drain launches as soon as the GPU is idle. */
+   max_batch/2 frags wait -- so under load batches grow to max_batch, up to
+   FD_ED25519_GPU_STAGE_DEPTH are outstanding and FD_ED25519_GPU_QUEUE_DEPTH
+   of them on the GPU (the pipelined kernel runs one phase of three of them
+   per launch, two launches queued behind), and at low load latency stays at
+   one batch: the stage's worker finishes a lone batch with drain launches
+   as soon as the GPU is idle. */
 
 #include "../../include/fd_ed25519_gpu.h"
 #include "../../include/fd_verify_offload.h"
@@ -32,7 +34,7 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
   if( !off || !ctx || !tc || !max_batch ) return FD_ED25519_GPU_ERR_ARG;
   fd_ed25519_gpu_stage_t * st = fd_ed25519_gpu_stage_new( ctx, tc, max_batch, threads );
   if( !st ) return FD_ED25519_GPU_ERR_OOM;
-  enum { DEPTH = FD_ED25519_GPU_QUEUE_DEPTH };   /* the stage's batches in flight */
+  enum { DEPTH = FD_ED25519_GPU_STAGE_DEPTH };   /* the stage's batches outstanding */
   uint64_t q_seq[ DEPTH ], q_cnt[ DEPTH ];   /* outstanding batches, oldest first */
   int q = 0;
   uint64_t done = fd_verify_offload_done_seq( off );

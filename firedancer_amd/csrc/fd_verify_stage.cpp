@@ -32,6 +32,9 @@
 
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <condition_variable>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -253,16 +256,22 @@ extern "C" int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t * ctx, int block );
 extern "C" int fd_ed25519_gpu_poll_block( fd_ed25519_gpu_t * ctx );
 extern "C" uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx );
 extern "C" int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n );
+/* hipHostRegister of [p, p + sz): 0 registered here, 1 the range was
+   registered already (by the caller), < 0 failed (fd_ed25519_gpu_host.cpp) */
+extern "C" int fd_ed25519_gpu_host_register_auto( fd_ed25519_gpu_t * ctx, void * p, uint64_t sz );
 
-/* Batches outstanding at once: the pipelined verify kernel's three phases
-   plus two queued launches (fd_ed25519_gpu_submit / fd_ed25519_gpu_frags_submit
-   take FD_ED25519_GPU_QUEUE_DEPTH and finish each one two launches after its
-   own; with only three, every blocking poll waited for the launch just
-   submitted and the GPU idled through each replay). */
-#define FD_VS_DEPTH FD_ED25519_GPU_QUEUE_DEPTH
+/* Batches outstanding at once: more than the GPU queue's
+   FD_ED25519_GPU_QUEUE_DEPTH (fd_ed25519_gpu_submit / _frags_submit take that
+   many: the pipelined kernel's three phases plus two queued launches, each
+   batch finished two launches after its own), so the completion worker
+   refills the GPU queue from the stage's waiting batches as soon as one
+   completes, before it replays it. */
+#define FD_VS_DEPTH FD_ED25519_GPU_STAGE_DEPTH
 
 struct vs_batch {
-  int                            state = 0; /* 0 free, 1 parsed, 2 on the GPU, 3 GPU done / nothing to verify */
+  int                            state = 0; /* 0 free, 1 parsed, 2 on the GPU, 3 GPU done / nothing to verify,
+                                               4 replayed (complete), 5 failed (err) */
+  int                            err   = 0; /* state 5: the status its poll returns */
   int                            devp  = 0; /* parsed on the GPU (fd_ed25519_gpu_frags_submit) */
   uint8_t const *                harena = nullptr;   /* devp: the caller's arena and frags */
   uint64_t                       harena_sz = 0;
@@ -280,15 +289,33 @@ struct vs_batch {
   std::vector<uint32_t>          fld;       /* per frag: sig_off, pub_off, msg_off, msg_sz (parallel parse) */
 };
 
+/* Host registrations the stage made of its callers' frag areas (page-locked
+   so the span copies are DMA, not staged copies on the calling thread);
+   released at stage_delete. */
+#define FD_VS_MAX_REG 8
+
 struct fd_ed25519_gpu_stage {
   fd_ed25519_gpu_t *        ctx;
   fd_ed25519_gpu_tcache_t * tc;
   uint64_t                  max_frags;
   int                       threads;
   int                       devparse;      /* parse frags on the GPU when the context has room */
+  int                       autoreg;       /* page-lock callers' frag areas (default on) */
   int                       head;          /* oldest pending slot */
   int                       pending;       /* 0..FD_VS_DEPTH */
   vs_batch                  b[ FD_VS_DEPTH ];
+  /* the completion worker: completes GPU batches in order and replays their
+     tcache steps while the caller's thread submits the next ones.  mu guards
+     the batch states and every call on ctx (which is not thread-safe); the
+     tcache and a batch's arrays belong to the worker from state 2 to 4. */
+  std::mutex                mu;
+  std::condition_variable   cv;            /* a batch completed (4 / 5) or work arrived for the worker */
+  std::thread               worker;
+  int                       stop;
+  struct { uint8_t const * p; uint64_t sz; } reg[ FD_VS_MAX_REG ];
+  int                       nreg;
+  uint32_t                  reg_foreign;   /* bit k: reg[k] was registered by the caller */
+  fd_ed25519_gpu_stage_stats_t stats;
 };
 
 /* Parse frags [lo, hi) of a batch into per-frag status / tag / count / fields. */
@@ -451,11 +478,16 @@ vs_replay( fd_ed25519_gpu_tcache_t * tc, vs_batch * b, int threads ) {
   }
 }
 
+static inline uint64_t vs_now( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 static int
 vs_launch( fd_ed25519_gpu_t * ctx, vs_batch * b, int threads ) {
   if( b->devp ) {
     int err = fd_ed25519_gpu_frags_submit( ctx, b->harena, b->harena_sz, b->hfrag, b->n, b->result, b->tag.data() );
-    if( err == FD_ED25519_GPU_ERR_BUSY ) return err;   /* both frag slots queued: stays parsed (state 1) */
+    if( err == FD_ED25519_GPU_ERR_BUSY ) return err;   /* every frag slot queued: stays parsed (state 1) */
     if( err != FD_ED25519_GPU_ERR_ARG ) {
       if( err ) return err;
       b->state = 2;
@@ -472,6 +504,106 @@ vs_launch( fd_ed25519_gpu_t * ctx, vs_batch * b, int threads ) {
   return FD_ED25519_GPU_OK;
 }
 
+/* Launch parsed batches (state 1) in submission order while the GPU side
+   takes them (it says BUSY when its queue of that kind is full, or while
+   batches of the other kind -- host vs device parse -- are pending).  A
+   batch whose launch fails is marked failed (state 5): its own poll reports
+   the error, in order.  Under st->mu. */
+static void
+vs_launch_ready( fd_ed25519_gpu_stage_t * st ) {
+  uint64_t t0 = vs_now();
+  for( int j=0; j<st->pending; j++ ) {
+    vs_batch * b = &st->b[ (st->head + j) % FD_VS_DEPTH ];
+    if( b->state != 1 ) continue;
+    int err = vs_launch( st->ctx, b, st->threads );
+    if( err == FD_ED25519_GPU_ERR_BUSY ) break;
+    if( err ) { b->err = err; b->state = 5; }
+  }
+  st->stats.launch_ns += vs_now() - t0;
+}
+
+/* The completion worker.  The oldest batch on the GPU (state 2) is polled
+   without blocking (a pipelined batch short of its phase C gets its drain
+   launches there once the GPU is idle), with the lock held only for the
+   poll; when its codes are in, the GPU queue has room again, so queued
+   batches are launched, and the tcache replay then runs outside the lock,
+   in batch order, while the caller submits.  Batches with nothing for the
+   GPU (state 3 from the launch) are replayed the same way, in order. */
+static void
+vs_worker( fd_ed25519_gpu_stage_t * st ) {
+  std::unique_lock<std::mutex> lk( st->mu );
+  uint64_t spin_t0 = 0;
+  for(;;) {
+    /* the oldest batch not yet complete */
+    vs_batch * b = NULL;
+    for( int j=0; j<st->pending; j++ ) {
+      vs_batch * x = &st->b[ (st->head + j) % FD_VS_DEPTH ];
+      if( x->state == 4 || x->state == 5 ) continue;
+      b = x;
+      break;
+    }
+    if( !b || b->state == 1 ) {
+      if( st->stop && !b ) return;
+      spin_t0 = 0;
+      st->cv.wait( lk );
+      continue;
+    }
+    if( b->state == 2 ) {
+      uint64_t t0 = vs_now();
+      int r = b->devp ? fd_ed25519_gpu_frags_poll( st->ctx, 0 ) : fd_ed25519_gpu_poll( st->ctx );
+      st->stats.gpu_poll_ns += vs_now() - t0;
+      if( r == FD_ED25519_GPU_PENDING ) {
+        /* the GPU is still at it: back off without the lock.  A batch is
+           ~0.6 ms of GPU work and the next launches wait for this one's
+           replay, so the worker spins (yielding) through a batch's time
+           and sleeps only once the GPU has been busy for 5 ms */
+        uint64_t t1 = vs_now();
+        if( !spin_t0 ) spin_t0 = t1;
+        lk.unlock();
+        if( t1 - spin_t0 < 5000000u ) std::this_thread::yield();
+        else { struct timespec ts = { 0, 20000 }; nanosleep( &ts, NULL ); }
+        lk.lock();
+        st->stats.gpu_wait_ns += vs_now() - t1;
+        continue;
+      }
+      spin_t0 = 0;
+      if( r != FD_ED25519_GPU_OK ) { b->err = r; b->state = 5; vs_launch_ready( st ); st->cv.notify_all(); continue; }
+      b->state = 3;
+      vs_launch_ready( st );                  /* the GPU queue has room again */
+    }
+    /* state 3: replay outside the lock (the tcache and b's arrays are the
+       worker's until the batch is marked complete) */
+    lk.unlock();
+    uint64_t t0 = vs_now();
+    vs_replay( st->tc, b, st->threads );
+    uint64_t dt = vs_now() - t0;
+    lk.lock();
+    st->stats.replay_ns += dt;
+    st->stats.batches++; st->stats.frags += b->n;
+    b->state = 4;
+    st->cv.notify_all();
+  }
+}
+
+/* Page-locks the caller's frag area once (hipHostRegister), so each span
+   copy to HBM is a DMA instead of a staged copy on the calling thread.  A
+   range the caller registered already (HIP says so) is fine as it is.  Best
+   effort: a failure leaves the area pageable. */
+static void
+vs_autoreg( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, uint64_t arena_sz ) {
+  if( !st->autoreg || !arena || !arena_sz ) return;
+  for( int k=0; k<st->nreg; k++ )
+    if( arena >= st->reg[ k ].p && arena + arena_sz <= st->reg[ k ].p + st->reg[ k ].sz ) return;
+  if( st->nreg == FD_VS_MAX_REG ) return;
+  uint64_t t0 = vs_now();
+  int r = fd_ed25519_gpu_host_register_auto( st->ctx, (void *)arena, arena_sz );
+  if( r >= 0 ) {
+    if( r ) st->reg_foreign |= 1u << st->nreg;          /* the caller's registration: never unregistered here */
+    st->reg[ st->nreg ].p = arena; st->reg[ st->nreg ].sz = arena_sz; st->nreg++;
+  }
+  st->stats.register_ns += vs_now() - t0;
+}
+
 extern "C" fd_ed25519_gpu_stage_t *
 fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, uint64_t max_frags, int threads ) {
   if( !ctx || !tc || !max_frags ) return NULL;
@@ -480,19 +612,27 @@ fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, 
   st->ctx = ctx; st->tc = tc; st->max_frags = max_frags;
   st->threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
   st->devparse = 1;
+  char const * e = getenv( "FD_ED25519_GPU_STAGE_AUTOREG" );        /* "0": leave frag areas pageable (A/B) */
+  st->autoreg = !(e && e[0] == '0');
+  memset( &st->stats, 0, sizeof(st->stats) );
   /* size the device-parse buffers now, not while a batch is in flight
      (best effort: a context too small for max_frags parses on the host) */
   if( max_frags <= fd_ed25519_gpu_frags_cap( ctx ) ) fd_ed25519_gpu_frags_reserve( ctx, max_frags );
+  try { st->worker = std::thread( vs_worker, st ); }
+  catch( ... ) { delete st; return NULL; }
   return st;
 }
 
 extern "C" int
 fd_ed25519_gpu_stage_warm( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, uint64_t arena_sz ) {
-  if( !st || st->pending || (!arena && arena_sz) ) return FD_ED25519_GPU_ERR_ARG;
+  if( !st || (!arena && arena_sz) ) return FD_ED25519_GPU_ERR_ARG;
+  std::lock_guard<std::mutex> lk( st->mu );
+  if( st->pending ) return FD_ED25519_GPU_ERR_ARG;
   uint64_t n = st->max_frags;
   if( !st->devparse || n > fd_ed25519_gpu_frags_cap( st->ctx ) ) return FD_ED25519_GPU_OK;
   static uint8_t const zero[ 64 ] = { 0 };
   if( !arena_sz ) { arena = zero; arena_sz = sizeof(zero); }
+  else vs_autoreg( st, arena, arena_sz );
   /* full-size throw-away batches of one repeated short frag (it fails the
      frag checks: no descriptors) through every slot */
   std::vector<fd_ed25519_gpu_frag_t> fr( n );
@@ -510,23 +650,16 @@ fd_ed25519_gpu_stage_warm( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, u
 extern "C" void
 fd_ed25519_gpu_stage_delete( fd_ed25519_gpu_stage_t * st ) {
   if( !st ) return;
-  while( st->pending ) if( fd_ed25519_gpu_stage_poll( st, 1 ) < 0 ) break;
-  delete st;
-}
-
-/* Launch parsed batches (state 1) in submission order while the GPU side
-   takes them (it says BUSY when its queue of that kind is full, or while
-   batches of the other kind -- host vs device parse -- are pending). */
-static int
-vs_launch_ready( fd_ed25519_gpu_stage_t * st ) {
-  for( int j=0; j<st->pending; j++ ) {
-    vs_batch * b = &st->b[ (st->head + j) % FD_VS_DEPTH ];
-    if( b->state != 1 ) continue;
-    int err = vs_launch( st->ctx, b, st->threads );
-    if( err == FD_ED25519_GPU_ERR_BUSY ) return FD_ED25519_GPU_OK;
-    if( err ) return err;
+  while( st->pending ) if( fd_ed25519_gpu_stage_poll( st, 1 ) < 0 && !st->pending ) break;
+  {
+    std::lock_guard<std::mutex> lk( st->mu );
+    st->stop = 1;
+    st->cv.notify_all();
   }
-  return FD_ED25519_GPU_OK;
+  st->worker.join();
+  for( int k=0; k<st->nreg; k++ )
+    if( !((st->reg_foreign >> k) & 1u) ) fd_ed25519_gpu_host_unregister( st->ctx, (void *)st->reg[ k ].p );
+  delete st;
 }
 
 extern "C" int
@@ -534,56 +667,82 @@ fd_ed25519_gpu_stage_submit( fd_ed25519_gpu_stage_t * st, uint8_t const * arena,
                              fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt, int8_t * result, uint64_t * sig ) {
   if( !st || (!frag && frag_cnt) || (frag_cnt && (!result || !sig)) || (!arena && arena_sz) ) return FD_ED25519_GPU_ERR_ARG;
   if( frag_cnt > st->max_frags ) return FD_ED25519_GPU_ERR_ARG;
-  if( st->pending == FD_VS_DEPTH ) return FD_ED25519_GPU_ERR_BUSY;
-  vs_batch * b = &st->b[ (st->head + st->pending) % FD_VS_DEPTH ];
-  b->result = result; b->sig = sig;
+  uint64_t t0 = vs_now();
+  vs_batch * b;
+  {
+    std::lock_guard<std::mutex> lk( st->mu );
+    if( st->pending == FD_VS_DEPTH ) return FD_ED25519_GPU_ERR_BUSY;
+    b = &st->b[ (st->head + st->pending) % FD_VS_DEPTH ];    /* free: only this thread fills it */
+  }
+  b->result = result; b->sig = sig; b->err = 0;
   b->devp = st->devparse && frag_cnt && frag_cnt <= fd_ed25519_gpu_frags_cap( st->ctx );
   if( b->devp ) {
     b->n = frag_cnt; b->harena = arena; b->harena_sz = arena_sz; b->hfrag = frag; b->ndesc = 0;
     b->tag.resize( frag_cnt );
   } else {
+    uint64_t tp = vs_now();
     vs_parse( b, arena, arena_sz, frag, frag_cnt, st->threads );
+    st->stats.parse_ns += vs_now() - tp;
   }
+  std::lock_guard<std::mutex> lk( st->mu );
+  if( b->devp ) vs_autoreg( st, arena, arena_sz );
   b->state = 1;
   st->pending++;
   /* straight to the GPU when its queue has room: with three batches in
      flight the pipelined kernel runs one phase of each per launch */
-  return vs_launch_ready( st );
+  vs_launch_ready( st );
+  st->cv.notify_all();
+  st->stats.submit_ns += vs_now() - t0;
+  return FD_ED25519_GPU_OK;
 }
 
 extern "C" int
 fd_ed25519_gpu_stage_poll( fd_ed25519_gpu_stage_t * st, int block ) {
   if( !st ) return FD_ED25519_GPU_ERR_ARG;
+  uint64_t t0 = vs_now();
+  std::unique_lock<std::mutex> lk( st->mu );
   if( !st->pending ) return FD_ED25519_GPU_OK;
   vs_batch * b = &st->b[ st->head ];
-  if( b->state == 1 ) { int err = vs_launch( st->ctx, b, st->threads ); if( err ) return err; }
-  if( b->state == 2 ) {
-    for(;;) {
-      int r = b->devp ? fd_ed25519_gpu_frags_poll( st->ctx, block ) : (block ? fd_ed25519_gpu_poll_block( st->ctx )
-                                                                                : fd_ed25519_gpu_poll( st->ctx ));
-      if( r == FD_ED25519_GPU_OK ) break;
-      if( r != FD_ED25519_GPU_PENDING ) { b->state = 0; st->pending--; st->head = (st->head + 1) % FD_VS_DEPTH; return r; }
-      if( !block ) return FD_ED25519_GPU_PENDING;
-      std::this_thread::yield();
-    }
-    b->state = 3;
+  while( b->state != 4 && b->state != 5 ) {
+    if( !block ) return FD_ED25519_GPU_PENDING;
+    st->cv.wait( lk );
   }
-  /* the GPU queue has room again: start the next parsed batches before the
-     host replays this one */
-  int err = vs_launch_ready( st );
-  vs_replay( st->tc, b, st->threads );
+  int err = b->state == 5 ? b->err : FD_ED25519_GPU_OK;
   b->state = 0;
   st->pending--;
   st->head = (st->head + 1) % FD_VS_DEPTH;
+  st->stats.poll_ns += vs_now() - t0;
   return err;
 }
 
 extern "C" int
-fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st ) { return st ? st->pending : 0; }
+fd_ed25519_gpu_stage_stats( fd_ed25519_gpu_stage_t * st, fd_ed25519_gpu_stage_stats_t * out ) {
+  if( !st || !out ) return FD_ED25519_GPU_ERR_ARG;
+  std::lock_guard<std::mutex> lk( st->mu );
+  *out = st->stats;
+  return FD_ED25519_GPU_OK;
+}
+
+extern "C" int
+fd_ed25519_gpu_stage_stats_reset( fd_ed25519_gpu_stage_t * st ) {
+  if( !st ) return FD_ED25519_GPU_ERR_ARG;
+  std::lock_guard<std::mutex> lk( st->mu );
+  memset( &st->stats, 0, sizeof(st->stats) );
+  return FD_ED25519_GPU_OK;
+}
+
+extern "C" int
+fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st ) {
+  if( !st ) return 0;
+  std::lock_guard<std::mutex> lk( ((fd_ed25519_gpu_stage_t *)st)->mu );
+  return st->pending;
+}
 
 extern "C" int
 fd_ed25519_gpu_stage_set_device_parse( fd_ed25519_gpu_stage_t * st, int on ) {
-  if( !st || st->pending ) return FD_ED25519_GPU_ERR_ARG;
+  if( !st ) return FD_ED25519_GPU_ERR_ARG;
+  std::lock_guard<std::mutex> lk( st->mu );
+  if( st->pending ) return FD_ED25519_GPU_ERR_ARG;
   st->devparse = !!on;
   return FD_ED25519_GPU_OK;
 }

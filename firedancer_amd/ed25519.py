@@ -6,8 +6,9 @@ import os
 import numpy as np
 
 # FD_ED25519_GPU_QUEUE_DEPTH (include/fd_ed25519_gpu.h): batches in flight for submit / poll
-# and the verify stage
 QUEUE_DEPTH = 5
+# FD_ED25519_GPU_STAGE_DEPTH: batches outstanding in the verify stage
+STAGE_DEPTH = 8
 
 FD_ED25519_SUCCESS = 0
 FD_ED25519_ERR_SIG = -1
@@ -75,6 +76,7 @@ def load_lib():
     lib.fd_ed25519_gpu_poll_block.argtypes = [vp]
     lib.fd_ed25519_gpu_pending.argtypes = [vp]
     lib.fd_ed25519_gpu_pipe_status.argtypes = [vp, i32]
+    lib.fd_ed25519_gpu_host_stats.argtypes = [vp, vp, i32]
     lib.fd_ed25519_gpu_test_ctab_stats.argtypes = [i32, vp, vp]
     lib.fd_ed25519_gpu_launch_stats.argtypes = [vp, vp, vp]
     lib.fd_ed25519_gpu_build_id.restype = ctypes.c_char_p
@@ -318,6 +320,18 @@ class Ed25519Gpu:
         if r == GPU_OK and self._keep:
             self._keep.popleft()
         return r == GPU_OK
+
+    _HOST_STATS = ("scan_ns", "stage_ns", "h2d_ns", "launch_ns", "out_ns", "h2d_bytes")
+
+    def host_stats(self, reset=False):
+        """fd_ed25519_gpu_host_stats: host time of the submit paths (ns) and the
+        bytes copied to HBM."""
+        import ctypes as C
+        buf = (C.c_uint64 * len(self._HOST_STATS))()
+        r = self.lib.fd_ed25519_gpu_host_stats(self.ctx, buf, 1 if reset else 0)
+        if r:
+            raise GpuError("fd_ed25519_gpu_host_stats: %s (%d)" % (strerror(r), r))
+        return dict(zip(self._HOST_STATS, list(buf)))
 
     def launch_stats(self):
         """(pipelined launches, one-shot launches) of this context so far."""

@@ -106,7 +106,8 @@ class VerifyStage:
 
 
 class AsyncStage:
-    """fd_ed25519_gpu_stage_*: up to QUEUE_DEPTH batches in flight, completed in order;
+    """fd_ed25519_gpu_stage_*: up to STAGE_DEPTH batches outstanding (QUEUE_DEPTH on the
+    GPU), completed in order by the stage's worker thread;
     frags parsed on the GPU by default (device_parse=False: on the host)."""
 
     def __init__(self, gpu, tcache, max_frags, threads=4, device_parse=True):
@@ -121,6 +122,8 @@ class AsyncStage:
         lib.fd_ed25519_gpu_stage_delete.argtypes = [vp]
         lib.fd_ed25519_gpu_stage_set_device_parse.argtypes = [vp, C.c_int]
         lib.fd_ed25519_gpu_stage_warm.argtypes = [vp, vp, C.c_uint64]
+        lib.fd_ed25519_gpu_stage_stats.argtypes = [vp, vp]
+        lib.fd_ed25519_gpu_stage_stats_reset.argtypes = [vp]
         self.lib, self.gpu, self.tcache = lib, gpu, tcache
         self.st = lib.fd_ed25519_gpu_stage_new(gpu.ctx, tcache.tc, max_frags, threads)
         if not self.st:
@@ -151,6 +154,22 @@ class AsyncStage:
 
     def pending(self):
         return int(self.lib.fd_ed25519_gpu_stage_pending(self.st))
+
+    _STATS = ("submit_ns", "parse_ns", "register_ns", "launch_ns", "poll_ns",
+              "gpu_poll_ns", "gpu_wait_ns", "replay_ns", "batches", "frags")
+
+    def stats(self, reset=False):
+        """fd_ed25519_gpu_stage_stats: where the stage's host time went (ns) --
+        the caller's submit / poll and the completion worker's GPU polls,
+        back-off waits and tcache replays."""
+        import ctypes as C
+        buf = (C.c_uint64 * len(self._STATS))()
+        r = self.lib.fd_ed25519_gpu_stage_stats(self.st, buf)
+        if r:
+            raise GpuError("fd_ed25519_gpu_stage_stats: %s (%d)" % (strerror(r), r))
+        if reset:
+            self.lib.fd_ed25519_gpu_stage_stats_reset(self.st)
+        return dict(zip(self._STATS, list(buf)))
 
     def warm(self, arena=None):
         """fd_ed25519_gpu_stage_warm: pay first-use costs (first DMA from a registered

@@ -49,6 +49,14 @@ extern "C" {
    replay, profiles/r03/stage_trace). */
 #define FD_ED25519_GPU_QUEUE_DEPTH 5
 
+/* Batches outstanding at once in the verify stage (fd_ed25519_gpu_stage_*):
+   more than the GPU queue holds, so the stage's completion worker has the
+   next batches at hand and refills the GPU queue the moment a batch
+   completes, without waiting for the caller's next submit
+   (profiles/r04/stage_trace: with the stage at the queue's depth, the GPU
+   sat idle before 28 of 32 batches waiting for the caller). */
+#define FD_ED25519_GPU_STAGE_DEPTH 8
+
 /* Infrastructure status (return values) */
 #define FD_ED25519_GPU_OK          (0)
 #define FD_ED25519_GPU_PENDING     (1)
@@ -94,6 +102,17 @@ fd_ed25519_gpu_t * fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch 
 fd_ed25519_gpu_t * fd_ed25519_gpu_new_devs( int const * dev_ids, int ndev, uint64_t max_batch );
 void               fd_ed25519_gpu_delete( fd_ed25519_gpu_t * ctx );
 int                fd_ed25519_gpu_device_cnt( fd_ed25519_gpu_t const * ctx );
+/* Host time of the submit paths (fd_ed25519_gpu_submit, the stage's frag
+   batches), ns cumulative: scan = the shard's arena span, stage = frag
+   records / rebased descriptors into page-locked staging, h2d = issuing the
+   copies to HBM (a pageable source makes this a staged, synchronous copy),
+   launch = kernel launches and events; out = codes / statuses copied to the
+   caller at poll; h2d_bytes = bytes sent.  reset != 0 zeroes them after
+   the read. */
+typedef struct {
+  uint64_t scan_ns, stage_ns, h2d_ns, launch_ns, out_ns, h2d_bytes;
+} fd_ed25519_gpu_host_stats_t;
+int                fd_ed25519_gpu_host_stats( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_host_stats_t * out, int reset );
 /* Metrics: verify kernel launches so far by kind (pipelined; one-shot,
    counting each chunk and each launch of the frags path). */
 int                fd_ed25519_gpu_launch_stats( fd_ed25519_gpu_t const * ctx, uint64_t * pipe_launches,
@@ -331,20 +350,28 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
                                  fd_ed25519_gpu_frag_t const * frag, uint64_t frag_cnt,
                                  int8_t * result, uint64_t * sig_out );
 
-/* Asynchronous, double-buffered form of the stage (the batching verify tile
-   of SURVEY.md §8(f) next-1): submit parses a batch of frags on the host (on
-   up to `threads` host threads) and hands it to the GPU if the GPU is free;
-   poll completes the OLDEST outstanding batch -- when its GPU work is done it
-   starts the next batch's GPU work, then replays the tcache steps for the
-   completed batch and fills its result / sig arrays -- and returns
-   FD_ED25519_GPU_OK, or FD_ED25519_GPU_PENDING (block == 0 only).  At most
-   FD_ED25519_GPU_QUEUE_DEPTH batches are outstanding (one more submit
-   returns FD_ED25519_GPU_ERR_BUSY): each goes to the GPU at submit, so the
-   pipelined kernel runs one phase of each per launch with two launches queued
-   behind, and the host parse and replay overlap the GPU.  Batches complete strictly in submission order, which keeps the
-   tile's frag order for the tcache.  The frag bytes and the result / sig
-   arrays of a batch must stay valid until its poll returns OK.  The stage
-   uses ctx's async pair: no other submit on ctx while batches are pending. */
+/* Asynchronous form of the stage (the batching verify tile of SURVEY.md
+   §8(f) next-1): submit hands a batch of frags to the GPU (parsed there, or
+   on up to `threads` host threads) when the GPU queue has room, and returns;
+   a completion worker thread owned by the stage completes GPU batches in
+   submission order and replays the tcache steps of each (filling its result
+   / sig arrays) while the caller's thread submits the next ones; poll
+   retires the OLDEST outstanding batch once the worker has completed it and
+   returns its status -- FD_ED25519_GPU_OK, an error for that batch only, or
+   FD_ED25519_GPU_PENDING (block == 0 only).  At most
+   FD_ED25519_GPU_STAGE_DEPTH batches are outstanding (one more submit
+   returns FD_ED25519_GPU_ERR_BUSY); up to FD_ED25519_GPU_QUEUE_DEPTH of them
+   are on the GPU at once (the pipelined kernel runs one phase of three of
+   them per launch with two launches queued behind), the rest wait in the
+   stage and go to the GPU as earlier ones complete.  Batches
+   complete strictly in submission order, which keeps the tile's frag order
+   for the tcache.  The frag bytes and the result / sig arrays of a batch
+   must stay valid until its poll returns.  By default the stage page-locks
+   each frag area it is given (once; released by stage_delete;
+   FD_ED25519_GPU_STAGE_AUTOREG=0 leaves it pageable), so the span copies
+   to HBM are DMA from the caller's memory.  The stage owns ctx while it
+   lives: no other call on ctx while batches are pending (the worker uses
+   it from its own thread). */
 typedef struct fd_ed25519_gpu_stage fd_ed25519_gpu_stage_t;
 
 fd_ed25519_gpu_stage_t * fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,
@@ -355,6 +382,20 @@ int  fd_ed25519_gpu_stage_submit ( fd_ed25519_gpu_stage_t * st, uint8_t const * 
                                    int8_t * result, uint64_t * sig );
 int  fd_ed25519_gpu_stage_poll   ( fd_ed25519_gpu_stage_t * st, int block );
 int  fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st );
+
+/* Where the stage's host time goes (ns, cumulative since stage_new or the
+   last reset): the caller's thread in submit (parse: host-parse batches
+   only; register: first-use page-locking of a frag area; launch: the GPU
+   launches and copies issued from submit and from the worker) and in poll
+   (waiting for the worker); the completion worker polling the GPU, backing
+   off while it runs, and replaying the tcache. */
+typedef struct {
+  uint64_t submit_ns, parse_ns, register_ns, launch_ns, poll_ns;
+  uint64_t gpu_poll_ns, gpu_wait_ns, replay_ns;
+  uint64_t batches, frags;
+} fd_ed25519_gpu_stage_stats_t;
+int  fd_ed25519_gpu_stage_stats      ( fd_ed25519_gpu_stage_t * st, fd_ed25519_gpu_stage_stats_t * out );
+int  fd_ed25519_gpu_stage_stats_reset( fd_ed25519_gpu_stage_t * st );
 /* By default the stage parses frags on the GPU (the frags' arena span is
    copied to HBM; parse, descriptor emission, verify and the per-frag fold
    run there; the host only replays the tcache), falling back to the host

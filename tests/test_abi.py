@@ -178,3 +178,5 @@ def test_queue_depth_mirror_matches_header():
     h = open(os.path.join(REPO, "include", "fd_ed25519_gpu.h")).read()
     m = re.search(r"#define FD_ED25519_GPU_QUEUE_DEPTH (\d+)", h)
     assert m and int(m.group(1)) == fa.QUEUE_DEPTH == 5
+    m = re.search(r"#define FD_ED25519_GPU_STAGE_DEPTH (\d+)", h)
+    assert m and int(m.group(1)) == fa.STAGE_DEPTH > fa.QUEUE_DEPTH

@@ -212,9 +212,11 @@ def test_pipe_scratch_all_or_nothing():
 
 def test_lsort_wait_expiry_is_reported():
     """A diagnostic build whose phase-A length-order waits expire at once
-    (tools/bin/lib_xlsort.so, -DFD_DIAG_LSORT_TIMEOUT): the launch must
-    report FD_ED25519_GPU_ERR_LAUNCH through the error word instead of
-    returning codes from a partial order."""
+    (tools/bin/lib_xlsort.so, -DFD_DIAG_LSORT_TIMEOUT): the pipelined batch
+    that hit it is reported (pipe_status / its poll: FD_ED25519_GPU_ERR_LAUNCH)
+    instead of returning codes from a partial order -- and ONLY that batch
+    (the error word used to fail every later call on the slot):
+    pipe_status clears, the one-shot kernels and later launches go on."""
     import ctypes
     path = os.path.join(REPO, "tools", "bin", "lib_xlsort.so")
     assert os.path.exists(path), "build tools/ (make -C tools) first"
@@ -226,11 +228,16 @@ def test_lsort_wait_expiry_is_reported():
     lib.fd_ed25519_gpu_pipe_flush_dev.argtypes = [vp, i32, vp]
     lib.fd_ed25519_gpu_pipe_status.argtypes = [vp, i32]
     lib.fd_ed25519_gpu_delete.argtypes = [vp]
+    lib.fd_ed25519_verify_batch_gpu.argtypes = [vp, vp, u64, vp, u64, vp]
+    lib.fd_ed25519_gpu_submit.argtypes = [vp, vp, u64, vp, u64, vp]
+    lib.fd_ed25519_gpu_poll_block.argtypes = [vp]
     recs = _golden()[:4096]                            # 16 full workgroups
     arena, desc, sz = fa.pack_batch([(r["msg"], r["sig"], r["pub"]) for r in recs])
+    want = np.array([r["code"] for r in recs], np.int8)
     d_arena = torch.from_numpy(arena.copy()).cuda()
     d_desc = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
     out = torch.zeros(len(recs), dtype=torch.int8, device="cuda:0")
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
     c = lib.fd_ed25519_gpu_new(1, 4096)
     assert c
     try:
@@ -240,8 +247,50 @@ def test_lsort_wait_expiry_is_reported():
         lib.fd_ed25519_gpu_pipe_flush_dev(c, 0, st)
         torch.cuda.synchronize()
         assert lib.fd_ed25519_gpu_pipe_status(c, 0) == -102          # FD_ED25519_GPU_ERR_LAUNCH
-        assert lib.fd_ed25519_gpu_pipe_dev(c, 0, d_arena.data_ptr(), sz, d_desc.data_ptr(), len(recs),
-                                           out.data_ptr(), st) == -102
+        assert lib.fd_ed25519_gpu_pipe_status(c, 0) == 0             # reported once, then cleared
+        # the one-shot kernels are unaffected by the pipe's failure
+        o1 = np.zeros(len(recs), np.int8)
+        assert lib.fd_ed25519_verify_batch_gpu(c, p(arena), sz, p(desc), len(recs), p(o1)) == 0
+        assert np.array_equal(o1, want)
+        # an async pipelined batch that hits it fails alone; the next one-shot call still verifies
+        o2 = np.zeros(len(recs), np.int8)
+        assert lib.fd_ed25519_gpu_submit(c, p(arena), sz, p(desc), len(recs), p(o2)) == 0
+        assert lib.fd_ed25519_gpu_poll_block(c) == -102
+        o3 = np.zeros(len(recs), np.int8)
+        assert lib.fd_ed25519_verify_batch_gpu(c, p(arena), sz, p(desc), len(recs), p(o3)) == 0
+        assert np.array_equal(o3, want)
     finally:
         torch.cuda.synchronize()
         lib.fd_ed25519_gpu_delete(c)
+
+
+def test_dev_and_async_pipe_calls_exclude_each_other(gpu):
+    """the _dev pipe entry and the async queues share the slot's
+    pipe state.  While a _dev batch sits between its phases, submit says BUSY
+    (its phase C would run with no copy-out on the queue's stream); while
+    async batches are pending, pipe_dev / pipe_flush_dev say BUSY.  Codes of
+    both kinds stay exact when they alternate."""
+    recs = _golden()[:1200]
+    a, d, sz, _, want = _host(recs)
+    d_arena = torch.from_numpy(a.copy()).cuda()
+    d_desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    out_dev = torch.full((len(recs),), 99, dtype=torch.int8, device="cuda:0")
+    st = torch.cuda.current_stream()
+    for rep in range(2):
+        gpu.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), len(recs), out_dev.data_ptr(), stream=st.cuda_stream)
+        out = np.full(len(recs), 99, np.int8)
+        with pytest.raises(fa.GpuError, match="-104"):
+            gpu.submit(a, sz, d, out)                       # a _dev batch holds the pipe
+        gpu.pipe_flush_dev(stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out_dev.cpu().numpy(), want)
+        gpu.submit(a, sz, d, out)
+        with pytest.raises(fa.GpuError, match="-104"):
+            gpu.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), len(recs), out_dev.data_ptr(),
+                         stream=st.cuda_stream)
+        with pytest.raises(fa.GpuError, match="-104"):
+            gpu.pipe_flush_dev(stream=st.cuda_stream)
+        assert gpu.poll(block=True)
+        assert np.array_equal(out, want)
+        # the synchronous one-shot call is not a pipe user
+        assert np.array_equal(gpu.verify_batch(a, sz, d), want)

@@ -323,8 +323,9 @@ def test_verify_frags_random_stream_vs_reference_tile(gpu, ref):
 @pytest.mark.parametrize("devparse", [1, 0])
 def test_stage_async_queue_depth_vs_reference_tile(gpu, ref, devparse):
     """The asynchronous stage (fd_ed25519_gpu_stage_*): batches of varying
-    size submitted with up to QUEUE_DEPTH outstanding (the pipelined kernel's
-    three phases + two queued launches), completed in order; results
+    size submitted with up to STAGE_DEPTH outstanding (QUEUE_DEPTH of them on
+    the GPU: the pipelined kernel's three phases + two queued launches; the
+    rest launched by the completion worker), completed in order; results
     equal the sequential reference tile's -- with the frags parsed on the GPU
     (default) and on the host."""
     import ctypes as C
@@ -368,7 +369,7 @@ def test_stage_async_queue_depth_vs_reference_tile(gpu, ref, devparse):
                 break
             assert lib.fd_ed25519_gpu_stage_poll(st, 1) == 0
         assert r == 0, r
-        assert lib.fd_ed25519_gpu_stage_pending(st) <= fa.QUEUE_DEPTH
+        assert lib.fd_ed25519_gpu_stage_pending(st) <= fa.STAGE_DEPTH
     while lib.fd_ed25519_gpu_stage_pending(st):
         assert lib.fd_ed25519_gpu_stage_poll(st, 1) == 0
     lib.fd_ed25519_gpu_stage_delete(st)

@@ -8,6 +8,7 @@ builds return the same codes.
 
 AB_MODE=pipe times fd_ed25519_gpu_pipe_dev launches (the bench's step) instead
 of the one-shot fd_ed25519_verify_batch_gpu_dev (codes checked after a flush).
+AB_MSG=var with n = 1048576: config 3's workload (one-shot launches).
 """
 import ctypes
 import os
@@ -21,9 +22,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402  (the bench's own synthetic workload)
 
-libs = [a for a in sys.argv[1:] if a.endswith(".so")]
-n = int(sys.argv[-1]) if not sys.argv[-1].endswith(".so") else 65536
-arena, desc, sz, expect, _ = bench.build_workload(n, 200, seed=0, n_keys=None)
+# a library argument may carry context settings: A.so@FD_ED25519_GPU_SL_LDS=4096
+# (environment set while that library's context is created)
+libs = [a for a in sys.argv[1:] if ".so" in a]
+n = int(sys.argv[-1]) if ".so" not in sys.argv[-1] else 65536
+# AB_MSG=var: config 3's Uniform{0..1232}-B messages (65,536 keys) instead of 200 B
+VAR = os.environ.get("AB_MSG") == "var"
+arena, desc, sz, expect, _ = bench.build_workload(n, None if VAR else 200, seed=0, n_keys=65536 if VAR else None)
 d_arena = torch.from_numpy(arena).cuda()
 d_desc = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
 outs = [torch.zeros(n, dtype=torch.int8, device="cuda") for _ in libs]
@@ -31,7 +36,12 @@ st = torch.cuda.Stream()
 torch.cuda.set_stream(st)
 vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
 ctx = []
-for p in libs:
+for spec in libs:
+    p, _, env = spec.partition("@")
+    saved = dict(os.environ)
+    if env:
+        k, _, v = env.partition("=")
+        os.environ[k] = v
     lib = ctypes.CDLL(os.path.abspath(p))
     lib.fd_ed25519_gpu_new.restype = vp
     lib.fd_ed25519_gpu_new.argtypes = [u64, u64]
@@ -40,6 +50,8 @@ for p in libs:
     lib.fd_ed25519_gpu_pipe_flush_dev.argtypes = [vp, i32, vp]
     c = lib.fd_ed25519_gpu_new(1, n)
     assert c, p
+    os.environ.clear()
+    os.environ.update(saved)
     ctx.append((lib, c))
 
 
@@ -58,7 +70,7 @@ for _ in range(30):
         launch(k)
 torch.cuda.synchronize()
 times = [[] for _ in libs]
-for rnd in range(14):
+for rnd in range(int(os.environ.get("AB_ROUNDS", "14"))):
     for k in range(len(libs)):
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
         for a, b in ev:
@@ -75,6 +87,7 @@ for k, p in enumerate(libs):
     # tools/bin/lib_x*.so: diagnostic builds with wrong results by design (timing only)
     if not os.path.basename(p).startswith("lib_x"):
         assert np.array_equal(outs[k].cpu().numpy(), expect), p
+    p = os.path.basename(p.partition("@")[0]) + ("@" + p.partition("@")[2] if "@" in p else "")
     t = sorted(times[k])
     print("%-50s median %.4f ms (%.2f M verifies/s) p10 %.4f p90 %.4f" % (
         os.path.basename(p), statistics.median(t), n / statistics.median(t) / 1e3, t[len(t) // 10], t[9 * len(t) // 10]),

@@ -102,50 +102,63 @@ def main():
     fr = np.ascontiguousarray(frags)
 
     def measure(pipe):
+        """(frags/s, results, launches, breakdown) of the async stage: with the
+        stage's default page-locking of the frag area, then with the frag
+        area left pageable (FD_ED25519_GPU_STAGE_AUTOREG=0)"""
         os.environ["FD_ED25519_GPU_ASYNC_PIPE"] = "1" if pipe else "0"
-        big = fa.Ed25519Gpu(device_mask=1, max_batch=16 * ab)
-        ast = fa.AsyncStage(big, fa.TCache(), ab, threads=8, device_parse=True)
-        res_a = np.zeros(len(frags), np.int8); sig_a = np.zeros(len(frags), np.uint64)
+        out = {}
+        for mode in ("registered", "pageable"):
+            if mode == "pageable":
+                os.environ["FD_ED25519_GPU_STAGE_AUTOREG"] = "0"
+            big = fa.Ed25519Gpu(device_mask=1, max_batch=16 * ab)
+            ast = fa.AsyncStage(big, fa.TCache(), ab, threads=8, device_parse=True)
+            os.environ.pop("FD_ED25519_GPU_STAGE_AUTOREG", None)
+            res_a = np.zeros(len(frags), np.int8); sig_a = np.zeros(len(frags), np.uint64)
+            calls = {"submit_s": 0.0, "poll_s": 0.0}
 
-        host = {"submit_s": 0.0, "poll_s": 0.0}
+            def run_async():
+                ast.tcache.reset()
+                i = 0
+                while i < len(fr) or ast.pending():
+                    if i < len(fr) and ast.pending() < fa.STAGE_DEPTH:
+                        j = min(len(fr), i + ab)
+                        t = time.perf_counter()
+                        ast.submit(arena, len(arena), fr[i:j], res_a[i:j], sig_a[i:j])
+                        calls["submit_s"] += time.perf_counter() - t
+                        i = j
+                    else:
+                        t = time.perf_counter()
+                        ast.poll(True)
+                        calls["poll_s"] += time.perf_counter() - t
 
-        def run_async():
-            ast.tcache.reset()
-            i = 0
-            while i < len(fr) or ast.pending():
-                if i < len(fr) and ast.pending() < fa.QUEUE_DEPTH:
-                    j = min(len(fr), i + ab)
-                    t = time.perf_counter()
-                    ast.submit(arena, len(arena), fr[i:j], res_a[i:j], sig_a[i:j])
-                    host["submit_s"] += time.perf_counter() - t
-                    i = j
-                else:
-                    t = time.perf_counter()
-                    ast.poll(True)
-                    host["poll_s"] += time.perf_counter() - t
-
-        def timed():
-            run_async()
+            run_async()                       # first use: registration, buffers
+            ast.stats(reset=True); big.host_stats(reset=True)
+            calls["submit_s"] = calls["poll_s"] = 0.0
             t = []
             for _ in range(args.steps):
                 t1 = time.perf_counter(); run_async(); t.append(time.perf_counter() - t1)
-            return float(np.mean(t))
-        dt_a = timed()
-        runs = args.steps + 1
-        host_ms = {"submit_ms_per_run": host["submit_s"] / runs * 1e3, "poll_ms_per_run": host["poll_s"] / runs * 1e3}
-        res_pageable = res_a.copy()
-        # the same with the frag area page-locked (a tile's dcache workspace is
-        # registered once: fd_ed25519_gpu_host_register)
-        big.host_register(arena)
-        dt_r = timed()
-        big.host_unregister(arena)
-        assert np.array_equal(res_a, res_pageable)
-        launches = big.launch_stats()
-        ast.close(); big.close()
+            dt_m = float(np.mean(t))
+            st, hs = ast.stats(), big.host_stats()
+            per = lambda ns: ns / args.steps / 1e6          # ms per run
+            out[mode] = {
+                "frags_per_s": args.frags / dt_m, "sigs_per_s": n_sigs / dt_m, "ms": dt_m * 1e3,
+                "caller_ms_per_run": {"submit": calls["submit_s"] / args.steps * 1e3,
+                                      "poll_wait": calls["poll_s"] / args.steps * 1e3},
+                "stage_ms_per_run": {k[:-3]: per(v) for k, v in st.items() if k.endswith("_ns")},
+                "submit_path_ms_per_run": {k[:-3]: per(v) for k, v in hs.items() if k.endswith("_ns")},
+                "h2d_gb_per_run": hs["h2d_bytes"] / args.steps / 1e9,
+                "batches_per_run": st["batches"] / args.steps,
+            }
+            if mode == "registered":
+                res_reg = res_a.copy()
+                launches = big.launch_stats()
+            else:
+                assert np.array_equal(res_a, res_reg)
+            ast.close(); big.close()
         os.environ.pop("FD_ED25519_GPU_ASYNC_PIPE", None)
-        return dt_a, dt_r, res_a, launches, host_ms
-    dt_a, dt_r, res_a, launches, host_a = measure(True)
-    dt_o, dt_or, res_o, launches_o, host_o = measure(False)
+        return out, res_reg, launches
+    pipe_m, res_a, launches = measure(True)
+    one_m, res_o, launches_o = measure(False)
     assert np.array_equal(res_a, res_o)
     line = {"metric": "verify-stage frags/sec (fd_ed25519_gpu_verify_frags, host frags)",
             "value": args.frags / dt, "unit": "frags/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -154,16 +167,14 @@ def main():
             "config": {"workload": "%d frags, %d signatures, tcache depth 16 / map 64" % (args.frags, n_sigs),
                        "arena_bytes": int(len(arena))},
             "sigs_per_s": n_sigs / dt, "host_parse_ms": parse_ms, "results": hist, "gen_s": gen_s,
-            "async_device_parse": {"frags_per_s": args.frags / dt_a, "ms": dt_a * 1e3, "batch": ab,
-                                   "in_flight": fa.QUEUE_DEPTH, "kernel": "pipelined", "launches_pipe_oneshot": launches,
-                                   "host_calls": host_a,
-                                   "registered_frags_per_s": args.frags / dt_r, "registered_ms": dt_r * 1e3,
-                                   "sigs_per_s": n_sigs / dt_a, "registered_sigs_per_s": n_sigs / dt_r,
-                                   "results": {int(k): int(v) for k, v in zip(*np.unique(res_a, return_counts=True))}},
-            "async_device_parse_oneshot": {"frags_per_s": args.frags / dt_o, "ms": dt_o * 1e3,
-                                           "registered_frags_per_s": args.frags / dt_or,
-                                           "sigs_per_s": n_sigs / dt_o, "registered_sigs_per_s": n_sigs / dt_or,
-                                           "launches_pipe_oneshot": launches_o,
+            "async_device_parse": {"batch": ab, "in_flight": fa.QUEUE_DEPTH, "stage_depth": fa.STAGE_DEPTH, "kernel": "pipelined",
+                                   "launches_pipe_oneshot": launches, **pipe_m,
+                                   "results": {int(k): int(v) for k, v in zip(*np.unique(res_a, return_counts=True))},
+                                   "note": "registered: the stage page-locks the frag area itself (default); "
+                                           "pageable: FD_ED25519_GPU_STAGE_AUTOREG=0.  stage_ms_per_run: the "
+                                           "caller's submit / poll and the completion worker's GPU polls, back-off "
+                                           "waits and tcache replays; submit_path_ms_per_run: inside the GPU submits"},
+            "async_device_parse_oneshot": {**one_m, "launches_pipe_oneshot": launches_o,
                                            "note": "FD_ED25519_GPU_ASYNC_PIPE=0: the same stage on the one-shot kernels"},
             "cpu_baseline": None if args.no_cpu else cpu_baseline(arena, frags)}
     print(json.dumps(line), flush=True)
