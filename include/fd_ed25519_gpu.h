@@ -576,6 +576,17 @@ void fd_ed25519_gpu_sha256( uint8_t const * msg, uint64_t sz, uint8_t out[ 32 ] 
    using it, *builds = tables this process has built so far. */
 int fd_ed25519_gpu_test_ctab_stats( int dev, uint64_t * refs, uint64_t * builds );
 
+/* Test hook (host only, no device): the copy plan the submit paths use for
+   a batch of n descriptors (kind 0, fd_ed25519_desc_t) or frags (kind 1,
+   fd_ed25519_gpu_frag_t) sharded contiguously over nslot slots: bytes[j] =
+   arena bytes slot j copies to HBM, runs[j] = its copies (page runs).  With
+   image != NULL, slot j's device arena image is also built at image + j *
+   image_cap (the runs at their packed offsets) and the items, rebased onto
+   their slot's image as the submit paths rebase them, go to rebased. */
+int fd_ed25519_gpu_test_copy_plan( int kind, void const * items, uint64_t n, uint8_t const * arena, uint64_t arena_sz,
+                                   int nslot, uint64_t * bytes, uint64_t * runs,
+                                   uint8_t * image, uint64_t image_cap, void * rebased );
+
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
    u32 words each, k < l) on the context's first device.  out: n records of

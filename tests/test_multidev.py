@@ -77,10 +77,33 @@ def test_sharded_async_submit_poll(mgpu):
     assert np.array_equal(out, np.array([r["code"] for r in recs], np.int8))
 
 
-def test_sharded_device_parse_stage_vs_reference_tile(mgpu):
+def _ring_relayout(arena, frags, ring_sz, start, chunk=64):
+    """The same frags laid out in a dcache-like ring of ring_sz bytes from
+    `start`: a frag that would cross the ring's end starts again at 0, so
+    the batch wraps (frag order != arena order).  fd_txn_t offsets are
+    payload-relative and chunks stay 64-B aligned, so every frag parses the
+    same."""
+    out = np.zeros(ring_sz, np.uint8)
+    fr = frags.copy()
+    pos = start
+    for i in range(len(frags)):
+        o, z = int(frags["off"][i]), int(frags["sz"][i])
+        if pos + z > ring_sz:
+            pos = 0
+        out[pos:pos + z] = arena[o:o + z]
+        fr["off"][i] = pos
+        pos += (z + chunk - 1) // chunk * chunk
+    assert pos < start
+    return out, fr
+
+
+@pytest.mark.parametrize("layout", ["packed", "wrapped_ring"])
+def test_sharded_device_parse_stage_vs_reference_tile(mgpu, layout):
     """The async verify stage with the frags parsed on the GPU, its frag batches
     sharded over the three slots (fd_ed25519_gpu_frags_submit), against the
-    sequential reference tile."""
+    sequential reference tile -- also with the frags in a wrapped dcache ring,
+    where each slot copies the page runs its shard occupies (cp_plan: two of
+    them for the slot holding the wrap) and parses rebased frag records."""
     import os
     import test_verify_stage as tvs
     if not os.path.exists(tvs.REF_SO):
@@ -90,6 +113,8 @@ def test_sharded_device_parse_stage_vs_reference_tile(mgpu):
                                            C.c_void_p, C.c_void_p]
     rng = np.random.default_rng(303)
     arena, frags = tvs._random_frag_stream(rng, 600, 1500)
+    if layout == "wrapped_ring":
+        arena, frags = _ring_relayout(arena, frags, len(arena) + (1 << 20), len(arena) // 2 + (1 << 20))
     exp_res, exp_tag = tvs.ref_seq(ref, arena, frags)
     lib = fa.load_lib()
     vp = C.c_void_p
@@ -125,6 +150,29 @@ def test_sharded_device_parse_stage_vs_reference_tile(mgpu):
     lib.fd_ed25519_gpu_stage_delete(st)
     bad = np.nonzero((res != exp_res) | (sig != exp_tag))[0]
     assert len(bad) == 0, [(int(j), int(res[j]), int(exp_res[j])) for j in bad[:10]]
+
+
+def test_sharded_far_fields_copy_runs(mgpu):
+    """fd_ed25519_gpu_submit over three slots with every public key in a key
+    area 48 MB past the signatures and messages: each slot copies its two
+    page runs (cp_plan), not a 48 MB span, and the rebased descriptors give
+    the golden codes."""
+    recs = _golden()
+    arena, desc, sz = fa.pack_batch([(r["msg"], r["sig"], r["pub"]) for r in recs])
+    far = 48 << 20
+    big = np.zeros(far + 32 * len(recs) + 64, np.uint8)
+    big[:sz] = arena[:sz]
+    d = desc.copy()
+    for j, r in enumerate(recs):
+        big[far + 32 * j:far + 32 * j + 32] = np.frombuffer(r["pub"], np.uint8)
+        d["pub_off"][j] = far + 32 * j
+    mgpu.host_stats(reset=True)
+    out = np.full(len(recs), 99, np.int8)
+    mgpu.submit(big, len(big), d, out)
+    assert mgpu.poll(block=True)
+    assert np.array_equal(out, np.array([r["code"] for r in recs], np.int8))
+    sent = mgpu.host_stats()["h2d_bytes"]
+    assert sent < sz + 32 * len(recs) + 16 * len(recs) + 3 * 4 * 2 * 4096 * 17, sent
 
 
 def test_sharded_keycache(mgpu):
