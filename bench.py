@@ -235,6 +235,95 @@ def shred_cpu_baseline(recs, budget_s):
                       % (done // len(recs), len(recs), dt)}
 
 
+def hostfed_main(args):
+    """--path host-fed: the verifier fed from HOST memory, PCIe in the loop
+    (VERDICT r03 next #3), one GPU, a line of its own (not the headline,
+    which is device-resident).  Measured: H2D copy bandwidth from page-locked
+    and from pageable memory; config 2 (64K x 200 B) and config 3 (1M,
+    Uniform{0..1232} B) through fd_ed25519_verify_batch_gpu (synchronous,
+    one-shot kernels: copy in, verify, codes out, one batch at a time) and
+    through fd_ed25519_gpu_submit / _poll (QUEUE_DEPTH batches of at most
+    64K in flight on the pipelined kernel, copies overlapping the kernels),
+    from a pageable and from a page-locked arena; bytes per verify (the
+    arena bytes the descriptors touch + the 16-B descriptor + the 1-B code)
+    and the link-bound ceiling they imply."""
+    import torch
+    import firedancer_amd as fa
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    out = {"metric": "host-fed Ed25519 verifies/sec (PCIe in the loop)", "unit": "verifies/s", "n_gpus": 1,
+           "data": "synthetic (tools/synth.py), all valid"}
+    # H2D bandwidth
+    nb = 256 << 20
+    h_pin = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h_page = np.ones(nb, np.uint8)
+    d_buf = torch.empty(nb, dtype=torch.uint8, device=dev)
+    bw = {}
+    for name, src in (("pinned", h_pin), ("pageable", torch.from_numpy(h_page))):
+        for _ in range(2):
+            d_buf.copy_(src, non_blocking=(name == "pinned"))
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(8):
+            d_buf.copy_(src, non_blocking=(name == "pinned"))
+        torch.cuda.synchronize()
+        bw[name] = 8 * nb / (time.perf_counter() - t) / 1e9
+    out["h2d_GBps"] = bw
+    del d_buf, h_pin, h_page
+    res = {}
+    for cfg, n, msg_sz in ((2, 65536, 200), (3, 1 << 20, None)):
+        arena, desc, sz, expect, data_desc = build_workload(n, msg_sz, seed=0, n_keys=min(n, 65536))
+        g = fa.Ed25519Gpu(device_mask=1, max_batch=min(n, 65536))
+        r = {"workload": data_desc, "bytes_per_verify": (sz + 17 * n) / n}
+        # synchronous one-shot calls over the whole batch (chunked by the library at max_batch)
+        assert np.array_equal(g.verify_batch(arena, sz, desc), expect)
+        t = time.perf_counter()
+        k = 3
+        for _ in range(k):
+            o = g.verify_batch(arena, sz, desc)
+        r["verify_batch_gpu_sync"] = k * n / (time.perf_counter() - t)
+        assert np.array_equal(o, expect)
+        # async pipelined stream of 64K batches, QUEUE_DEPTH in flight
+        bs = 65536
+        parts = [(i, min(bs, n - i)) for i in range(0, n, bs)]
+        reps = max(1, 16 * bs // n)
+
+        def stream():
+            outs = [np.zeros(c, np.int8) for _, c in parts] * reps
+            todo = [(i, c, outs[j]) for j, (i, c) in enumerate(parts * reps)]
+            pend = 0
+            t0 = time.perf_counter()
+            for i, c, o in todo:
+                while pend >= fa.QUEUE_DEPTH:
+                    assert g.poll(block=True); pend -= 1
+                g.submit(arena, sz, desc[i:i + c], o)
+                pend += 1
+            while pend:
+                assert g.poll(block=True); pend -= 1
+            dt = time.perf_counter() - t0
+            assert all(np.array_equal(o, expect[i:i + c]) for (i, c, o) in todo)
+            return len(todo) and sum(c for _, c, _ in todo) / dt
+        stream()
+        r["submit_poll_pageable"] = stream()
+        g.host_register(arena)
+        stream()
+        g.host_stats(reset=True)
+        r["submit_poll_registered"] = stream()
+        hs = g.host_stats()
+        r["submit_path_ms_registered"] = {k[:-3]: v / 1e6 for k, v in hs.items() if k.endswith("_ns")}
+        r["h2d_bytes_per_verify_registered"] = hs["h2d_bytes"] / (n * reps)
+        g.host_unregister(arena)
+        r["link_bound_verifies_per_s_pinned"] = bw["pinned"] * 1e9 / r["bytes_per_verify"]
+        g.close()
+        res["config%d" % cfg] = r
+    out["configs"] = res
+    out["value"] = res["config2"]["submit_poll_registered"]
+    out["note"] = ("value: config 2 through submit/poll from a page-locked arena; the headline line's value is "
+                   "device-resident.  link_bound = pinned H2D GB/s / bytes_per_verify")
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def shred_main(args):
     """--path shred: shreds/s through fd_ed25519_gpu_shred_verify (the
     FEC resolver's first-shred check as a descriptor source).
@@ -356,12 +445,14 @@ def main():
                          "fd_ed25519_gpu_verify_batch_dev launch (the whole batch); -1 (default): 1 when the batch "
                          "is at most one wave per SIMD (256 x CUs signatures: config 2), else 0 (larger batches "
                          "already give every SIMD several waves, and the single-lane kernel packs them better)")
-    ap.add_argument("--path", default="verify", choices=["verify", "shred"],
+    ap.add_argument("--path", default="verify", choices=["verify", "shred", "host-fed"],
                     help="verify (default): the headline line above.  shred: the FEC resolver's first-shred check "
                          "(fd_ed25519_gpu_shred_verify: host walk, Merkle roots on the GPU, verify) over the "
                          "reference's demo capture tiled to --batch, from host memory, N=1; a line of its own "
                          "(not the headline metric) with the host-hash variant and the reference's one-core check "
-                         "(oracle/_ref fdref_shred_check) beside it")
+                         "(oracle/_ref fdref_shred_check) beside it.  host-fed: configs 2 and 3 from HOST memory "
+                         "(sync calls and the async submit/poll stream, pageable and page-locked) beside the H2D "
+                         "bandwidth, N=1, a line of its own")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test mode (tests/test_bench_launch.py): gloo, a no-op step on a fixed count; "
                          "exercises the launcher, rank setup and SUM/MAX aggregation without a GPU")
@@ -382,6 +473,11 @@ def main():
             print("bench.py: --path shred runs on one GPU", file=sys.stderr, flush=True)
             sys.exit(2)
         sys.exit(shred_main(args))
+    if args.path == "host-fed":
+        if world != 1:
+            print("bench.py: --path host-fed runs on one GPU", file=sys.stderr, flush=True)
+            sys.exit(2)
+        sys.exit(hostfed_main(args))
 
     import torch
     import torch.distributed as dist

@@ -263,7 +263,7 @@ extern "C" int fd_ed25519_gpu_host_register_auto( fd_ed25519_gpu_t * ctx, void *
 /* Batches outstanding at once: more than the GPU queue's
    FD_ED25519_GPU_QUEUE_DEPTH (fd_ed25519_gpu_submit / _frags_submit take that
    many: the pipelined kernel's three phases plus two queued launches, each
-   batch finished two launches after its own), so the completion worker
+   batch finished two launches after its own), so the poller thread
    refills the GPU queue from the stage's waiting batches as soon as one
    completes, before it replays it. */
 #define FD_VS_DEPTH FD_ED25519_GPU_STAGE_DEPTH
@@ -304,13 +304,14 @@ struct fd_ed25519_gpu_stage {
   int                       head;          /* oldest pending slot */
   int                       pending;       /* 0..FD_VS_DEPTH */
   vs_batch                  b[ FD_VS_DEPTH ];
-  /* the completion worker: completes GPU batches in order and replays their
-     tcache steps while the caller's thread submits the next ones.  mu guards
-     the batch states and every call on ctx (which is not thread-safe); the
-     tcache and a batch's arrays belong to the worker from state 2 to 4. */
+  /* the worker threads (vs_poller, vs_replayer): GPU completions in order,
+     then the tcache replays in order, while the caller's thread submits.
+     mu guards the batch states and every call on ctx (which is not
+     thread-safe); the tcache and a batch's arrays belong to the replayer
+     from state 3 to 4. */
   std::mutex                mu;
-  std::condition_variable   cv;            /* a batch completed (4 / 5) or work arrived for the worker */
-  std::thread               worker;
+  std::condition_variable   cv;            /* any batch state change (all three threads wait on it) */
+  std::thread               poller, replayer;
   int                       stop;
   struct { uint8_t const * p; uint64_t sz; } reg[ FD_VS_MAX_REG ];
   int                       nreg;
@@ -522,57 +523,71 @@ vs_launch_ready( fd_ed25519_gpu_stage_t * st ) {
   st->stats.launch_ns += vs_now() - t0;
 }
 
-/* The completion worker.  The oldest batch on the GPU (state 2) is polled
-   without blocking (a pipelined batch short of its phase C gets its drain
-   launches there once the GPU is idle), with the lock held only for the
-   poll; when its codes are in, the GPU queue has room again, so queued
-   batches are launched, and the tcache replay then runs outside the lock,
-   in batch order, while the caller submits.  Batches with nothing for the
-   GPU (state 3 from the launch) are replayed the same way, in order. */
+/* The stage's two worker threads.  The poller completes GPU batches in
+   order: the oldest batch on the GPU (state 2) is polled without blocking
+   (a pipelined batch short of its phase C gets its drain launches there
+   once the GPU is idle), the lock held only for the poll; when its codes
+   are in, the GPU queue has room again and the waiting batches are
+   launched at once.  The replayer takes completed batches (state 3) in
+   order and replays their tcache steps outside the lock -- the only
+   sequential host work per frag -- so replay, launching and the caller's
+   submits overlap one another and the GPU (profiles/r04/stage: with one
+   worker doing both, its replay plus launches were the whole wall time). */
 static void
-vs_worker( fd_ed25519_gpu_stage_t * st ) {
+vs_poller( fd_ed25519_gpu_stage_t * st ) {
   std::unique_lock<std::mutex> lk( st->mu );
   uint64_t spin_t0 = 0;
   for(;;) {
-    /* the oldest batch not yet complete */
-    vs_batch * b = NULL;
+    vs_batch * b = NULL;                       /* the oldest batch still short of its GPU codes */
     for( int j=0; j<st->pending; j++ ) {
       vs_batch * x = &st->b[ (st->head + j) % FD_VS_DEPTH ];
-      if( x->state == 4 || x->state == 5 ) continue;
-      b = x;
-      break;
+      if( x->state == 1 || x->state == 2 ) { b = x; break; }
     }
     if( !b || b->state == 1 ) {
-      if( st->stop && !b ) return;
+      if( st->stop && !st->pending ) return;
       spin_t0 = 0;
       st->cv.wait( lk );
       continue;
     }
-    if( b->state == 2 ) {
-      uint64_t t0 = vs_now();
-      int r = b->devp ? fd_ed25519_gpu_frags_poll( st->ctx, 0 ) : fd_ed25519_gpu_poll( st->ctx );
-      st->stats.gpu_poll_ns += vs_now() - t0;
-      if( r == FD_ED25519_GPU_PENDING ) {
-        /* the GPU is still at it: back off without the lock.  A batch is
-           ~0.6 ms of GPU work and the next launches wait for this one's
-           replay, so the worker spins (yielding) through a batch's time
-           and sleeps only once the GPU has been busy for 5 ms */
-        uint64_t t1 = vs_now();
-        if( !spin_t0 ) spin_t0 = t1;
-        lk.unlock();
-        if( t1 - spin_t0 < 5000000u ) std::this_thread::yield();
-        else { struct timespec ts = { 0, 20000 }; nanosleep( &ts, NULL ); }
-        lk.lock();
-        st->stats.gpu_wait_ns += vs_now() - t1;
-        continue;
-      }
-      spin_t0 = 0;
-      if( r != FD_ED25519_GPU_OK ) { b->err = r; b->state = 5; vs_launch_ready( st ); st->cv.notify_all(); continue; }
-      b->state = 3;
-      vs_launch_ready( st );                  /* the GPU queue has room again */
+    uint64_t t0 = vs_now();
+    int r = b->devp ? fd_ed25519_gpu_frags_poll( st->ctx, 0 ) : fd_ed25519_gpu_poll( st->ctx );
+    st->stats.gpu_poll_ns += vs_now() - t0;
+    if( r == FD_ED25519_GPU_PENDING ) {
+      /* the GPU is still at it: back off without the lock.  A batch is
+         ~0.6 ms of GPU work, so the poller spins (yielding) through a
+         batch's time and sleeps only once the GPU has been busy for 5 ms */
+      uint64_t t1 = vs_now();
+      if( !spin_t0 ) spin_t0 = t1;
+      lk.unlock();
+      if( t1 - spin_t0 < 5000000u ) std::this_thread::yield();
+      else { struct timespec ts = { 0, 20000 }; nanosleep( &ts, NULL ); }
+      lk.lock();
+      st->stats.gpu_wait_ns += vs_now() - t1;
+      continue;
     }
-    /* state 3: replay outside the lock (the tcache and b's arrays are the
-       worker's until the batch is marked complete) */
+    spin_t0 = 0;
+    if( r != FD_ED25519_GPU_OK ) { b->err = r; b->state = 5; }
+    else b->state = 3;
+    vs_launch_ready( st );                     /* the GPU queue has room again */
+    st->cv.notify_all();
+  }
+}
+
+static void
+vs_replayer( fd_ed25519_gpu_stage_t * st ) {
+  std::unique_lock<std::mutex> lk( st->mu );
+  for(;;) {
+    vs_batch * b = NULL;                       /* the oldest batch not yet complete */
+    for( int j=0; j<st->pending; j++ ) {
+      vs_batch * x = &st->b[ (st->head + j) % FD_VS_DEPTH ];
+      if( x->state != 4 && x->state != 5 ) { b = x; break; }
+    }
+    if( !b || b->state != 3 ) {
+      if( st->stop && !st->pending ) return;
+      st->cv.wait( lk );
+      continue;
+    }
+    /* the tcache and b's arrays are the replayer's until b is complete */
     lk.unlock();
     uint64_t t0 = vs_now();
     vs_replay( st->tc, b, st->threads );
@@ -618,8 +633,15 @@ fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, 
   /* size the device-parse buffers now, not while a batch is in flight
      (best effort: a context too small for max_frags parses on the host) */
   if( max_frags <= fd_ed25519_gpu_frags_cap( ctx ) ) fd_ed25519_gpu_frags_reserve( ctx, max_frags );
-  try { st->worker = std::thread( vs_worker, st ); }
-  catch( ... ) { delete st; return NULL; }
+  try {
+    st->poller = std::thread( vs_poller, st );
+    st->replayer = std::thread( vs_replayer, st );
+  } catch( ... ) {
+    { std::lock_guard<std::mutex> lk( st->mu ); st->stop = 1; st->cv.notify_all(); }
+    if( st->poller.joinable() ) st->poller.join();
+    delete st;
+    return NULL;
+  }
   return st;
 }
 
@@ -637,9 +659,10 @@ fd_ed25519_gpu_stage_warm( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, u
      frag checks: no descriptors) through every slot */
   std::vector<fd_ed25519_gpu_frag_t> fr( n );
   for( uint64_t i=0; i<n; i++ ) { fr[ i ].off = 0u; fr[ i ].sz = (uint32_t)(arena_sz < 64u ? arena_sz : 64u); }
-  std::vector<int8_t> status( (size_t)FD_VS_DEPTH * n ); std::vector<uint64_t> tag( (size_t)FD_VS_DEPTH * n );
+  std::vector<int8_t> status( (size_t)FD_ED25519_GPU_QUEUE_DEPTH * n );
+  std::vector<uint64_t> tag( (size_t)FD_ED25519_GPU_QUEUE_DEPTH * n );
   int err = FD_ED25519_GPU_OK, queued = 0;
-  for( int k=0; k<FD_VS_DEPTH && !err; k++ ) {
+  for( int k=0; k<FD_ED25519_GPU_QUEUE_DEPTH && !err; k++ ) {       /* every GPU frag slot once */
     err = fd_ed25519_gpu_frags_submit( st->ctx, arena, arena_sz, fr.data(), n, status.data() + k * n, tag.data() + k * n );
     queued += !err;
   }
@@ -656,7 +679,8 @@ fd_ed25519_gpu_stage_delete( fd_ed25519_gpu_stage_t * st ) {
     st->stop = 1;
     st->cv.notify_all();
   }
-  st->worker.join();
+  st->poller.join();
+  st->replayer.join();
   for( int k=0; k<st->nreg; k++ )
     if( !((st->reg_foreign >> k) & 1u) ) fd_ed25519_gpu_host_unregister( st->ctx, (void *)st->reg[ k ].p );
   delete st;

@@ -107,7 +107,7 @@ class VerifyStage:
 
 class AsyncStage:
     """fd_ed25519_gpu_stage_*: up to STAGE_DEPTH batches outstanding (QUEUE_DEPTH on the
-    GPU), completed in order by the stage's worker thread;
+    GPU), completed in order by the stage's poller and replayer threads;
     frags parsed on the GPU by default (device_parse=False: on the host)."""
 
     def __init__(self, gpu, tcache, max_frags, threads=4, device_parse=True):
@@ -160,7 +160,7 @@ class AsyncStage:
 
     def stats(self, reset=False):
         """fd_ed25519_gpu_stage_stats: where the stage's host time went (ns) --
-        the caller's submit / poll and the completion worker's GPU polls,
+        the caller's submit / poll, the poller's GPU polls and
         back-off waits and tcache replays."""
         import ctypes as C
         buf = (C.c_uint64 * len(self._STATS))()

@@ -50,7 +50,7 @@ extern "C" {
 #define FD_ED25519_GPU_QUEUE_DEPTH 5
 
 /* Batches outstanding at once in the verify stage (fd_ed25519_gpu_stage_*):
-   more than the GPU queue holds, so the stage's completion worker has the
+   more than the GPU queue holds, so the stage's poller thread has the
    next batches at hand and refills the GPU queue the moment a batch
    completes, without waiting for the caller's next submit
    (profiles/r04/stage_trace: with the stage at the queue's depth, the GPU
@@ -353,10 +353,11 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
 /* Asynchronous form of the stage (the batching verify tile of SURVEY.md
    §8(f) next-1): submit hands a batch of frags to the GPU (parsed there, or
    on up to `threads` host threads) when the GPU queue has room, and returns;
-   a completion worker thread owned by the stage completes GPU batches in
-   submission order and replays the tcache steps of each (filling its result
-   / sig arrays) while the caller's thread submits the next ones; poll
-   retires the OLDEST outstanding batch once the worker has completed it and
+   two worker threads owned by the stage complete GPU batches in submission
+   order (the poller, which also launches waiting batches as the GPU queue
+   frees) and replay the tcache steps of each, in order, filling its result
+   / sig arrays (the replayer), while the caller's thread submits the next
+   ones; poll retires the OLDEST outstanding batch once it is replayed and
    returns its status -- FD_ED25519_GPU_OK, an error for that batch only, or
    FD_ED25519_GPU_PENDING (block == 0 only).  At most
    FD_ED25519_GPU_STAGE_DEPTH batches are outstanding (one more submit
@@ -370,7 +371,7 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
    each frag area it is given (once; released by stage_delete;
    FD_ED25519_GPU_STAGE_AUTOREG=0 leaves it pageable), so the span copies
    to HBM are DMA from the caller's memory.  The stage owns ctx while it
-   lives: no other call on ctx while batches are pending (the worker uses
+   lives: no other call on ctx while batches are pending (the poller uses
    it from its own thread). */
 typedef struct fd_ed25519_gpu_stage fd_ed25519_gpu_stage_t;
 
@@ -386,9 +387,9 @@ int  fd_ed25519_gpu_stage_pending( fd_ed25519_gpu_stage_t const * st );
 /* Where the stage's host time goes (ns, cumulative since stage_new or the
    last reset): the caller's thread in submit (parse: host-parse batches
    only; register: first-use page-locking of a frag area; launch: the GPU
-   launches and copies issued from submit and from the worker) and in poll
-   (waiting for the worker); the completion worker polling the GPU, backing
-   off while it runs, and replaying the tcache. */
+   launches and copies issued from submit and from the poller) and in poll
+   (waiting for the replayer); the poller polling the GPU and backing off
+   while it runs; the replayer replaying the tcache. */
 typedef struct {
   uint64_t submit_ns, parse_ns, register_ns, launch_ns, poll_ns;
   uint64_t gpu_poll_ns, gpu_wait_ns, replay_ns;

@@ -9,15 +9,14 @@ and the assembler (firedancer_amd/Makefile):
      issue_probe.json).  Same operation, same operands; only rewritten when
      S0 is a register or an inline constant (VOP3 takes no literal here).
 
-  2. The s_nop 0 the compiler places after each inline-asm block (it cannot
-     see inside asm and pads conservatively) is dropped when the block holds
-     only v_mad_u64_u32 / v_lshrrev_b64 (the field-product chains of
-     fd_f25519_dev.h) or the limb-pair / mask / negation helpers
-     (v_lshl_add_u64, v_lshlrev_b64, v_bfi_b32, v_xad_u32) and the next instruction is a plain ALU op from the
-     whitelist below -- the same pairs the compiler itself emits back to back
-     with no wait state when it generates those instructions.
+  (Rounds 1-3 also dropped the s_nop 0 the compiler places after each
+  inline-asm block when the next instruction was on a whitelist; a
+  same-process A/B in round 4 measured it within noise -- 0.5466 ms per
+  pipelined step with the drop, 0.5457 without, profiles/r04/ab/
+  ab_b2b_peephole_snop.log -- so the compiler's hazard padding now stays
+  as it emits it.)
 
-  3. Experimental rewrites for same-process A/Bs, off unless named in the
+  2. Experimental rewrites for same-process A/Bs, off unless named in the
      environment variable FD_PEEP (comma-separated):
        add2   v_lshlrev_b32_e32 D, 1, S      ->  v_add_u32_e32 D, S, S
               (same result; the add is one of the opcodes two waves of a
@@ -33,16 +32,6 @@ import re
 import sys
 
 INLINE_FLOAT = {"0.5", "-0.5", "1.0", "-1.0", "2.0", "-2.0", "4.0", "-4.0", "0.15915494"}
-SAFE_AFTER_ASM = {
-    "v_and_b32_e32", "v_and_b32_e64", "v_lshrrev_b64", "v_lshlrev_b64", "v_add_u32_e32", "v_add_u32_e64",
-    "v_sub_u32_e32", "v_sub_u32_e64", "v_mad_u64_u32", "v_mov_b32_e32", "v_mov_b64_e32", "v_lshl_add_u64",
-    "v_mul_lo_u32", "v_lshlrev_b32_e32", "v_lshrrev_b32_e32", "v_add3_u32", "v_alignbit_b32",
-    "v_mul_u32_u24_e32", "v_mad_u32_u24", "v_or_b32_e32", "v_xor_b32_e32", "v_bfi_b32", "v_xad_u32",
-    "v_lshl_add_u32", "v_cndmask_b32_e64", "v_bitop3_b32", "v_perm_b32",
-}
-ASM_BODY_OK = {"v_mad_u64_u32", "v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64", "v_bfi_b32", "v_xad_u32"}
-
-
 def is_inline_or_reg(op):
     op = op.strip()
     if re.fullmatch(r"-?[vs]\d+", op) or re.fullmatch(r"[vs]\[\d+:\d+\]", op):
@@ -93,35 +82,12 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     lines = open(src).read().split("\n")
     out = []
-    n_cnd = n_nop = 0
+    n_cnd = 0
     n_exp = {}
     i = 0
-    in_asm = False
-    asm_ok = True
-    last_asm_end = -10
     while i < len(lines):
         ln = lines[i]
         st = ln.strip()
-        if st.startswith(";;#ASMSTART"):
-            in_asm, asm_ok = True, True
-        elif st.startswith(";;#ASMEND"):
-            in_asm = False
-            last_asm_end = len(out)
-            out.append(ln)
-            i += 1
-            # drop a following s_nop 0 when safe
-            if asm_ok and i < len(lines) and lines[i].strip() == "s_nop 0":
-                j = i + 1
-                while j < len(lines) and mnemonic(lines[j]) is None and not lines[j].strip().endswith(":"):
-                    j += 1
-                if j < len(lines) and mnemonic(lines[j]) in SAFE_AFTER_ASM:
-                    n_nop += 1
-                    i += 1
-            continue
-        elif in_asm:
-            m = mnemonic(ln)
-            if m is not None and m not in ASM_BODY_OK:
-                asm_ok = False
         ln, k = experimental( ln )
         if k:
             n_exp[ k ] = n_exp.get( k, 0 ) + 1
@@ -132,8 +98,8 @@ def main():
         out.append(ln)
         i += 1
     open(dst, "w").write("\n".join(out))
-    sys.stderr.write("asm_peephole: %d v_cndmask_b32_e32 -> e64, %d s_nop after asm dropped%s\n" % (
-        n_cnd, n_nop, "".join(", %d %s" % (v, k) for k, v in sorted(n_exp.items()))))
+    sys.stderr.write("asm_peephole: %d v_cndmask_b32_e32 -> e64%s\n" % (
+        n_cnd, "".join(", %d %s" % (v, k) for k, v in sorted(n_exp.items()))))
 
 
 if __name__ == "__main__":
