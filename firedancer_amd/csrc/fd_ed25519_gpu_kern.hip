@@ -263,10 +263,18 @@ __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint6
   if( w[0] == 0xdeadbeefu && w[1] == 0xdeadbeefu ) m[0] = make_uint4( w[2], w[3], w[4], w[5] );
   return;
 #endif
+#if defined(FD_DIAG_NT_TABLES)   /* diagnostic: the table stores nontemporal */
+  typedef unsigned int u32x4 __attribute__(( ext_vector_type( 4 ) ));
+#pragma unroll
+  for( int j=0; j<8; j++ ) { u32x4 v = { w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] }; __builtin_nontemporal_store( v, (u32x4 *)m + j ); }
+#pragma unroll
+  for( int j=0; j<2; j++ ) { u32x4 v = { w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] }; __builtin_nontemporal_store( v, (u32x4 *)tl + j ); }
+#else
 #pragma unroll
   for( int j=0; j<8; j++ ) m[j] = make_uint4( w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
 #pragma unroll
   for( int j=0; j<2; j++ ) tl[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
+#endif
 }
 
 /* Table [0..8](-Q) for an affine Q (Z = 1), cached form (replaces the
@@ -1313,6 +1321,15 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   uint4 *    buf = s_buf[ role ][ wv ];
   uint32_t * y   = s_y[ role ][ wv ];
   bool phb = role == 1;
+#if defined(FD_DIAG_NT_INV)   /* diagnostic: invalidate this CU's vector L1 (1), the XCC's L2 (2) or both (3) first */
+#if FD_DIAG_NT_INV == 1
+  asm volatile( "buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory" );
+#elif FD_DIAG_NT_INV == 2
+  asm volatile( "buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" );
+#else
+  asm volatile( "buffer_inv sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" );
+#endif
+#endif
   uint64_t nx = phb ? a.n_b : a.n_c;
   if( (gid & ~(uint64_t)63) >= nx ) return;
   uint64_t set = phb ? a.set_b : a.set_c;

@@ -121,6 +121,13 @@ __device__ __forceinline__ uint64_t fe_shr25( uint64_t c ) {
   uint64_t r; asm( "v_lshrrev_b64 %0, 25, %1" : "=v"(r) : "v"(c) ); return r;
 }
 
+/* (uint32_t)(a >> 26) for a < 2^58 as ONE v_alignbit_b32 (left to itself
+   the compiler sometimes makes it a 64-bit shift plus a 64-bit add and a
+   move, in the squaring loops) */
+__device__ __forceinline__ uint32_t fe_hi26( uint64_t a ) {
+  uint32_t r; asm( "v_alignbit_b32 %0, %1, %2, 26" : "=v"(r) : "v"((uint32_t)(a >> 32)), "v"((uint32_t)a) ); return r;
+}
+
 /* column accumulators -> limbs (R form): mask, then fold the carry out of
    limb 9 (< 2^38) times 19 into limbs 0/1 */
 __device__ __forceinline__ void fe_finish( fe & h, uint64_t c0, uint64_t c1, uint64_t c2, uint64_t c3, uint64_t c4,
@@ -135,7 +142,7 @@ __device__ __forceinline__ void fe_finish( fe & h, uint64_t c0, uint64_t c1, uin
   uint64_t add = ((uint64_t)(19u*(uint32_t)(t>>32)) << 32) | (uint64_t)h0;
   uint64_t a = (uint64_t)(uint32_t)t * 19u + add;
   h0 = (uint32_t)a & FE_M26;
-  h1 += (uint32_t)(a >> 26);
+  h1 += fe_hi26( a );
   h.v[0]=h0; h.v[1]=h1; h.v[2]=h2; h.v[3]=h3; h.v[4]=h4; h.v[5]=h5; h.v[6]=h6; h.v[7]=h7; h.v[8]=h8; h.v[9]=h9;
 }
 
@@ -156,7 +163,7 @@ __device__ __forceinline__ void fe_finish_neg( fe & h, uint64_t c0, uint64_t c1,
   uint64_t add = ((uint64_t)(19u*(uint32_t)(t>>32)) << 32) | (uint64_t)h0;
   uint64_t a = (uint64_t)(uint32_t)t * 19u + add;
   h.v[0] = fe_bfi_not( (uint32_t)a, FE_M26 );
-  h.v[1] = fe_bfi_not( (uint32_t)c1, FE_M25 ) + ((1u << 25) - (uint32_t)(a >> 26));
+  h.v[1] = fe_bfi_not( (uint32_t)c1, FE_M25 ) + ((1u << 25) - fe_hi26( a ));
   h.v[2] = fe_bfi_not( (uint32_t)c2, FE_M26 ); h.v[3] = fe_bfi_not( (uint32_t)c3, FE_M25 );
   h.v[4] = fe_bfi_not( (uint32_t)c4, FE_M26 ); h.v[5] = fe_bfi_not( (uint32_t)c5, FE_M25 );
   h.v[6] = fe_bfi_not( (uint32_t)c6, FE_M26 ); h.v[7] = fe_bfi_not( (uint32_t)c7, FE_M25 );
