@@ -152,13 +152,20 @@ struct fparse_args {
   uint64_t                       n;
   int8_t *                       status;     /* out: 0 / FD_TXN_VERIFY_FAILED / _BAD_FRAG, then the fold */
   uint64_t *                     tag;        /* out */
-  uint32_t *                     cnt;        /* out: descriptors per frag, then (scan) their first index */
+  uint32_t *                     cnt;        /* out: first descriptor index, workgroup-relative */
   uint32_t *                     fld;        /* out: 4 per frag: sig, pub, msg offsets (span-relative), msg_sz */
-  uint32_t *                     total;      /* scan: descriptor count */
+  uint32_t *                     bpre;       /* out: per workgroup, its first descriptor index */
+  uint32_t *                     done;       /* workgroups finished (0 between launches) */
+  uint32_t *                     total;      /* out: descriptor count */
   fd_ed25519_desc_t *            desc;       /* emit: descriptors */
   uint64_t                       desc_cap;
   int8_t const *                 code;       /* fold: per-descriptor codes */
+  int8_t *                       hstatus;    /* fold: page-locked host staging (device-mapped) */
+  uint64_t *                     htag;
 };
+
+/* Frags per workgroup of the parse / emit / fold kernels. */
+#define FD_FRAG_BLOCK 256u
 
 /* Shred Merkle roots on the GPU (fd_shred_root_kernel, fd_shred_verify.cpp):
    one job per shred whose signature is checked -- the leaf is SHA-256 of
@@ -193,7 +200,6 @@ struct shred_root_args {
 #define FD_KERN_KPART    "fd_ed25519_kcache_part_kernel"
 #define FD_KERN_CACHED   "fd_ed25519_verify_cached_kernel"
 #define FD_KERN_FPARSE   "fd_frag_parse_kernel"
-#define FD_KERN_FSCAN    "fd_frag_scan_kernel"
 #define FD_KERN_FEMIT    "fd_frag_emit_kernel"
 #define FD_KERN_FFOLD    "fd_frag_fold_kernel"
 #define FD_KERN_PIPE     "fd_ed25519_verify_pipe_kernel"

@@ -263,7 +263,19 @@ __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint6
   if( w[0] == 0xdeadbeefu && w[1] == 0xdeadbeefu ) m[0] = make_uint4( w[2], w[3], w[4], w[5] );
   return;
 #endif
-#if defined(FD_DIAG_NT_TABLES)   /* diagnostic: the table stores nontemporal */
+#if defined(FD_DIAG_SC_TABLES)   /* diagnostic: the table stores at system scope (sc0 sc1) */
+  typedef unsigned int u32x4 __attribute__(( ext_vector_type( 4 ) ));
+#pragma unroll
+  for( int j=0; j<8; j++ ) {
+    u32x4 v = { w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] };
+    asm volatile( "global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"((uint64_t)(m + j)), "v"(v) : "memory" );
+  }
+#pragma unroll
+  for( int j=0; j<2; j++ ) {
+    u32x4 v = { w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] };
+    asm volatile( "global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"((uint64_t)(tl + j)), "v"(v) : "memory" );
+  }
+#elif defined(FD_DIAG_NT_TABLES)   /* diagnostic: the table stores nontemporal */
   typedef unsigned int u32x4 __attribute__(( ext_vector_type( 4 ) ));
 #pragma unroll
   for( int j=0; j<8; j++ ) { u32x4 v = { w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] }; __builtin_nontemporal_store( v, (u32x4 *)m + j ); }
@@ -1377,6 +1389,9 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       FE_FENCE();
     }
     stA = (int)((m_aok >> lane) & 1u) | (int)(((m_asm >> lane) & 1u) << 1);
+#if defined(FD_DIAG_SC_INV_AFTER)   /* diagnostic: this XCC's L2 invalidated once the tables are stored */
+    asm volatile( "s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" );
+#endif
     code = verify_precode( args, desc_ok, bad_s, stA, stR );
     if( valid ) a.code_b[ gid ] = (int8_t)code;
   } else {
@@ -1821,11 +1836,39 @@ fd_ed25519_verify_cached_kernel( verify_args args ) {
    BAD_FRAG here. */
 __device__ __forceinline__ uint32_t span_ld16( uint8_t const * p ) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
-extern "C" __global__ void __launch_bounds__( 256 )
+/* Exclusive prefix sum over the FD_FRAG_BLOCK threads of a workgroup
+   (wavefront scan by lane shifts, then the four wave totals through LDS);
+   *tot gets the workgroup's sum.  Every thread of the workgroup calls it. */
+__device__ __forceinline__ uint32_t frag_block_scan( uint32_t x, uint32_t * wsum, uint32_t * tot ) {
+  uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t v = x;
+#pragma unroll
+  for( uint32_t o=1u; o<64u; o<<=1 ) { uint32_t y = __shfl_up( v, o, 64 ); if( lane >= o ) v += y; }
+  __syncthreads();                                   /* wsum free (a previous call's readers done) */
+  if( lane == 63u ) wsum[ w ] = v;
+  __syncthreads();
+  uint32_t pre = 0u, all = 0u;
+#pragma unroll
+  for( uint32_t k=0; k<FD_FRAG_BLOCK/64u; k++ ) { pre += k < w ? wsum[ k ] : 0u; all += wsum[ k ]; }
+  *tot = all;
+  return pre + v - x;
+}
+
+/* The per-frag parse plus the descriptor-index scan in one launch (the
+   separate single-workgroup scan kernel took 44 us of a 35K-frag batch,
+   profiles/r04/stage): each workgroup writes its frags' workgroup-relative
+   first descriptor index into cnt and its descriptor total into bpre; the
+   last workgroup to finish (a device-scope counter, reset by that workgroup
+   for the next batch) turns bpre into the workgroups' first indices and
+   writes the batch's total.  Frag i's first descriptor is then
+   cnt[i] + bpre[i / FD_FRAG_BLOCK].  No workgroup waits for another. */
+extern "C" __global__ void __launch_bounds__( FD_FRAG_BLOCK )
 fd_frag_parse_kernel( fparse_args a ) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if( i >= a.n ) return;
-  fd_ed25519_gpu_frag_t f = a.frag[ i ];
+  __shared__ uint32_t wsum[ FD_FRAG_BLOCK / 64u ];
+  __shared__ uint32_t is_last;
+  uint64_t i = (uint64_t)blockIdx.x * FD_FRAG_BLOCK + threadIdx.x;
+  fd_ed25519_gpu_frag_t f; f.off = 0xffffffffu; f.sz = 0u;
+  if( i < a.n ) f = a.frag[ i ];
   int st = FD_TXN_VERIFY_BAD_FRAG;
   uint64_t tag = 0u;
   uint32_t cnt = 0u, so = 0u, po = 0u, mo = 0u, ms = 0u;
@@ -1851,58 +1894,48 @@ fd_frag_parse_kernel( fparse_args a ) {
     if( s_ + 64u*c > a.span_sz || p_ + 32u*c > a.span_sz ) break;
     st = 0; cnt = (uint32_t)c; so = (uint32_t)s_; po = (uint32_t)p_; mo = (uint32_t)(ro + m_); ms = (uint32_t)(psz - m_);
   } while( 0 );
-  a.status[ i ] = (int8_t)st; a.tag[ i ] = tag; a.cnt[ i ] = cnt;
-  uint32_t * fl = a.fld + 4u*i;
-  fl[0] = so; fl[1] = po; fl[2] = mo; fl[3] = ms;
+  uint32_t btot;
+  uint32_t excl = frag_block_scan( cnt, wsum, &btot );
+  if( i < a.n ) {
+    a.status[ i ] = (int8_t)st; a.tag[ i ] = tag; a.cnt[ i ] = excl;
+    uint4 fl; fl.x = so; fl.y = po; fl.z = mo; fl.w = ms;
+    ((uint4 *)a.fld)[ i ] = fl;
+  }
+  if( threadIdx.x == 0u ) {
+    a.bpre[ blockIdx.x ] = btot;
+    /* release: this workgroup's total is visible before the count says so;
+       acquire: the last one sees every workgroup's total */
+    uint32_t old = __hip_atomic_fetch_add( a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT );
+    is_last = old == gridDim.x - 1u;
+  }
+  __syncthreads();
+  if( !is_last ) return;
+  __threadfence();
+  uint32_t run = 0u;
+  for( uint32_t b0=0; b0<gridDim.x; b0+=FD_FRAG_BLOCK ) {
+    uint32_t j = b0 + threadIdx.x;
+    uint32_t v = j < gridDim.x ? a.bpre[ j ] : 0u;
+    uint32_t ctot;
+    uint32_t e = frag_block_scan( v, wsum, &ctot );
+    if( j < gridDim.x ) a.bpre[ j ] = run + e;
+    run += ctot;
+  }
+  if( threadIdx.x == 0u ) { *a.total = run; *a.done = 0u; }
 }
 
-/* Exclusive prefix sum of cnt[0, n) in place, total -> *a.total.  One
-   workgroup of 1024 threads: per-thread chunk sums, an LDS scan of the 1024
-   partials, then each thread rewrites its chunk. */
-extern "C" __global__ void __launch_bounds__( 1024 )
-fd_frag_scan_kernel( fparse_args a ) {
-  __shared__ uint32_t part[ 1024 ];
-  uint32_t t = threadIdx.x;
-  uint64_t per = (a.n + 1023u) / 1024u;
-  uint64_t lo = (uint64_t)t * per, hi = min( a.n, lo + per );
-  /* the chunk's counts in rounds of 16 independent loads (a rolled loop
-     waited one memory round trip per count: 53 us for a 32K-frag batch,
-     profiles/r04/stage_trace) */
-  uint32_t sum = 0u;
-  for( uint64_t i0=lo; i0<hi; i0+=16u ) {
-    uint32_t v[ 16 ];
-#pragma unroll
-    for( int j=0; j<16; j++ ) v[j] = i0 + (uint64_t)j < hi ? a.cnt[ i0 + (uint64_t)j ] : 0u;
-#pragma unroll
-    for( int j=0; j<16; j++ ) sum += v[j];
-  }
-  part[ t ] = sum;
-  __syncthreads();
-  for( uint32_t o=1u; o<1024u; o<<=1 ) {
-    uint32_t v = t >= o ? part[ t - o ] : 0u;
-    __syncthreads();
-    part[ t ] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[ t ] - sum;                 /* exclusive */
-  for( uint64_t i0=lo; i0<hi; i0+=16u ) {
-    uint32_t v[ 16 ];
-#pragma unroll
-    for( int j=0; j<16; j++ ) v[j] = i0 + (uint64_t)j < hi ? a.cnt[ i0 + (uint64_t)j ] : 0u;
-#pragma unroll
-    for( int j=0; j<16; j++ ) if( i0 + (uint64_t)j < hi ) { a.cnt[ i0 + (uint64_t)j ] = run; run += v[j]; }
-  }
-  if( t == 1023u ) *a.total = part[ 1023 ];
+/* Frag i's first descriptor index (i == n: the batch's total). */
+__device__ __forceinline__ uint64_t frag_first( fparse_args const & a, uint64_t i ) {
+  return i < a.n ? (uint64_t)a.cnt[ i ] + (uint64_t)a.bpre[ i / FD_FRAG_BLOCK ] : (uint64_t)*a.total;
 }
 
 /* Descriptors of every frag at its scanned position (txn_idx = frag index). */
-extern "C" __global__ void __launch_bounds__( 256 )
+extern "C" __global__ void __launch_bounds__( FD_FRAG_BLOCK )
 fd_frag_emit_kernel( fparse_args a ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= a.n || a.status[ i ] ) return;
   uint32_t const * fl = a.fld + 4u*i;
-  uint64_t at = a.cnt[ i ];
-  uint32_t c = (uint32_t)((i + 1u < a.n ? (uint64_t)a.cnt[ i + 1u ] : (uint64_t)*a.total) - at);
+  uint64_t at = frag_first( a, i );
+  uint32_t c = (uint32_t)(frag_first( a, i + 1u ) - at);
   for( uint32_t j=0; j<c && at + j < a.desc_cap; j++ ) {
     fd_ed25519_desc_t d;
     d.sig_off = fl[0] + 64u*j; d.pub_off = fl[1] + 32u*j; d.msg_off = fl[2];
@@ -1914,20 +1947,26 @@ fd_frag_emit_kernel( fparse_args a ) {
 /* Each frag's verify code from its descriptors' codes, with
    fd_ed25519_verify_batch_single_msg's precedence (first phase-1 error,
    else ERR_MSG, else SUCCESS), into status[i] for frags that had
-   descriptors. */
-extern "C" __global__ void __launch_bounds__( 256 )
+   descriptors; every frag's status and tag then go straight into the
+   host's page-locked staging (hstatus, htag: no copy launches after the
+   fold -- two of them plus their queue gaps were ~45 us a batch). */
+extern "C" __global__ void __launch_bounds__( FD_FRAG_BLOCK )
 fd_frag_fold_kernel( fparse_args a ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if( i >= a.n || a.status[ i ] ) return;
-  uint64_t at = a.cnt[ i ];
-  uint64_t end = i + 1u < a.n ? (uint64_t)a.cnt[ i + 1u ] : (uint64_t)*a.total;
-  int first = 0, any_msg = 0;
-  for( uint64_t k=at; k<end; k++ ) {
-    int c = a.code[ k ];
-    if( c == FD_ED25519_ERR_MSG ) any_msg = 1;
-    else if( c != FD_ED25519_SUCCESS && !first ) first = c;
+  if( i >= a.n ) return;
+  int st = a.status[ i ];
+  if( !st ) {
+    uint64_t at = frag_first( a, i ), end = frag_first( a, i + 1u );
+    int first = 0, any_msg = 0;
+    for( uint64_t k=at; k<end; k++ ) {
+      int c = a.code[ k ];
+      if( c == FD_ED25519_ERR_MSG ) any_msg = 1;
+      else if( c != FD_ED25519_SUCCESS && !first ) first = c;
+    }
+    st = first ? first : (any_msg ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS);
   }
-  a.status[ i ] = (int8_t)(first ? first : (any_msg ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS));
+  a.hstatus[ i ] = (int8_t)st;
+  a.htag[ i ] = a.tag[ i ];
 }
 
 /* Self-test kernel (tests only, fd_ed25519_gpu_test_lattice): the device

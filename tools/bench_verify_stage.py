@@ -131,6 +131,21 @@ def main():
                         ast.poll(True)
                         calls["poll_s"] += time.perf_counter() - t
 
+            def run_stream(reps):
+                """reps passes over the frags as ONE stream (no drain between
+                passes, like a tile that never stops): the 16-deep tcache has
+                forgotten a pass's frags long before they come again"""
+                ast.tcache.reset()
+                total, k = reps * len(fr), 0
+                while k < total or ast.pending():
+                    if k < total and ast.pending() < fa.STAGE_DEPTH:
+                        i = k % len(fr)
+                        j = min(len(fr), i + ab)
+                        ast.submit(arena, len(arena), fr[i:j], res_a[i:j], sig_a[i:j])
+                        k += j - i
+                    else:
+                        ast.poll(True)
+
             run_async()                       # first use: registration, buffers
             ast.stats(reset=True); big.host_stats(reset=True)
             calls["submit_s"] = calls["poll_s"] = 0.0
@@ -152,6 +167,12 @@ def main():
             if mode == "registered":
                 res_reg = res_a.copy()
                 launches = big.launch_stats()
+                t1 = time.perf_counter(); run_stream(args.steps); dt_s = time.perf_counter() - t1
+                diff = int(np.count_nonzero(res_a != res_reg))
+                assert diff <= 16, diff       # only a pass's first frags can meet the previous pass's last 16 tags
+                out["streaming"] = {"frags_per_s": args.steps * args.frags / dt_s,
+                                    "sigs_per_s": args.steps * n_sigs / dt_s, "ms_per_pass": dt_s / args.steps * 1e3,
+                                    "passes": args.steps, "results_differing_from_single_pass": diff}
             else:
                 assert np.array_equal(res_a, res_reg)
             ast.close(); big.close()
@@ -173,7 +194,9 @@ def main():
                                    "note": "registered: the stage page-locks the frag area itself (default); "
                                            "pageable: FD_ED25519_GPU_STAGE_AUTOREG=0.  stage_ms_per_run: the "
                                            "caller's submit / poll and the completion worker's GPU polls, back-off "
-                                           "waits and tcache replays; submit_path_ms_per_run: inside the GPU submits"},
+                                           "waits and tcache replays; submit_path_ms_per_run: inside the GPU submits; "
+                                           "streaming: --steps passes over the frags as one stream, no pipeline "
+                                           "fill / drain between passes (registered)"},
             "async_device_parse_oneshot": {**one_m, "launches_pipe_oneshot": launches_o,
                                            "note": "FD_ED25519_GPU_ASYNC_PIPE=0: the same stage on the one-shot kernels"},
             "cpu_baseline": None if args.no_cpu else cpu_baseline(arena, frags)}
