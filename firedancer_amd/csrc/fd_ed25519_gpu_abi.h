@@ -166,6 +166,11 @@ struct fparse_args {
 
 /* Frags per workgroup of the parse / emit / fold kernels. */
 #define FD_FRAG_BLOCK 256u
+/* Bytes of frag per signature at least: each signature's 64 bytes and its
+   signer's 32-byte address lie in the frag's payload (fd_txn_parse output),
+   so a frag of sz bytes holds at most sz / 96 signatures; the parse makes a
+   frag claiming more BAD_FRAG and the host sizes the verify grid by it. */
+#define FD_FRAG_SIG_BYTES 96u
 
 /* Shred Merkle roots on the GPU (fd_shred_root_kernel, fd_shred_verify.cpp):
    one job per shred whose signature is checked -- the leaf is SHA-256 of

@@ -1891,6 +1891,7 @@ fd_frag_parse_kernel( fparse_args a ) {
     for( int b=7; b>=0; b-- ) tag = (tag << 8) | sg[b];
     if( m_ > psz ) break;
     if( !c || c > 16u ) { st = FD_TXN_VERIFY_FAILED; break; }                  /* batch_sz 0 or > 16 -> ERR_SIG */
+    if( c * FD_FRAG_SIG_BYTES > sz ) break;                                     /* more signatures than the frag holds */
     if( s_ + 64u*c > a.span_sz || p_ + 32u*c > a.span_sz ) break;
     st = 0; cnt = (uint32_t)c; so = (uint32_t)s_; po = (uint32_t)p_; mo = (uint32_t)(ro + m_); ms = (uint32_t)(psz - m_);
   } while( 0 );

@@ -38,6 +38,7 @@
 #include <new>
 #include <thread>
 #include <vector>
+#include <immintrin.h>
 
 #include "../../include/fd_ed25519_gpu.h"
 
@@ -110,6 +111,114 @@ tc_insert( fd_ed25519_gpu_tcache_t * tc, uint64_t tag ) {
   tc->oldest = tc->oldest + 1u >= tc->depth ? 0u : tc->oldest + 1u;
   tc_remove( tc->map, tc->map_cnt, evict );
   return 0;
+}
+
+/* fd_txn_verify's tcache steps for one frag (fd_verify.h:63-86) with one
+   probe: the query's stopping slot is where an insert would put the tag
+   (nothing changes the map in between), so a verified frag is inserted
+   there without probing again.  1: present (DEDUP), 0: inserted, -1: not
+   verified (FAILED, nothing inserted). */
+static inline int
+tc_query_insert( fd_ed25519_gpu_tcache_t * tc, uint64_t tag, int ok ) {
+  uint64_t slot;
+  if( tc_probe( tc->map, tc->map_cnt, tag, &slot ) ) return 1;
+  if( !ok ) return -1;
+  tc->map[ slot ] = tag;
+  uint64_t evict = tc->ring[ tc->oldest ];
+  tc->ring[ tc->oldest ] = tag;
+  tc->oldest = tc->oldest + 1u >= tc->depth ? 0u : tc->oldest + 1u;
+  tc_remove( tc->map, tc->map_cnt, evict );
+  return 0;
+}
+
+/* The map of a tcache whose ring is given, rebuilt: the ring's tags
+   inserted oldest first into an empty map.  Linear probing with
+   backward-shift deletion (Knuth's Algorithm R, which tc_remove is) leaves
+   the table as if a removed key had never been inserted, so this is the map
+   the sequence of inserts and evictions would have left -- slot for slot
+   (tests/test_verify_stage.py::test_tcache_steps_ring_form_vs_reference). */
+static void
+tc_map_rebuild( fd_ed25519_gpu_tcache_t * tc ) {
+  memset( tc->map, 0, tc->map_cnt * sizeof(uint64_t) );
+  for( uint64_t k=0; k<tc->depth; k++ ) {
+    uint64_t t = tc->ring[ (tc->oldest + k) % tc->depth ];
+    if( !t ) continue;
+    uint64_t slot;
+    tc_probe( tc->map, tc->map_cnt, t, &slot );
+    tc->map[ slot ] = t;
+  }
+}
+
+/* The replay's tcache steps for a tcache of depth <= 4 * NR: the ring in NR
+   AVX2 registers (the present set is exactly the ring's nonzero tags, plus
+   the tag 0), a query is NR compares, an insert NR blends, no branches on
+   the map; the map is rebuilt once at the end of the batch.  The map form
+   (tc_query_insert) costs ~12 ns a frag on the GPU box's host, most of it
+   in the backward-shift removal, and it is the replay thread's whole work. */
+template<int NR>
+__attribute__((target("avx2"))) static void
+vs_replay_ring( fd_ed25519_gpu_tcache_t * tc, int8_t * res, uint64_t const * tg, uint64_t * sig, uint64_t n ) {
+  uint64_t depth = tc->depth, old = tc->oldest;
+  alignas(32) uint64_t buf[ 4 * NR ];
+  memset( buf, 0, sizeof(buf) );
+  memcpy( buf, tc->ring, depth * sizeof(uint64_t) );
+  __m256i r[ NR ], idx[ NR ];
+  for( int j=0; j<NR; j++ ) {
+    r[ j ]   = _mm256_load_si256( (__m256i const *)(buf + 4*j) );
+    idx[ j ] = _mm256_setr_epi64x( 4*j, 4*j + 1, 4*j + 2, 4*j + 3 );
+  }
+  for( uint64_t i=0; i<n; i++ ) {
+    int8_t v = res[ i ];
+    uint64_t tag = tg[ i ];
+    sig[ i ] = 0u;
+    if( v == FD_TXN_VERIFY_BAD_FRAG ) continue;
+    __m256i t = _mm256_set1_epi64x( (long long)tag );
+    __m256i hit = _mm256_cmpeq_epi64( r[ 0 ], t );
+    for( int j=1; j<NR; j++ ) hit = _mm256_or_si256( hit, _mm256_cmpeq_epi64( r[ j ], t ) );
+    if( !_mm256_testz_si256( hit, hit ) || !tag ) { res[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
+    if( v != FD_ED25519_SUCCESS )                 { res[ i ] = FD_TXN_VERIFY_FAILED; continue; }
+    __m256i o = _mm256_set1_epi64x( (long long)old );
+    for( int j=0; j<NR; j++ ) r[ j ] = _mm256_blendv_epi8( r[ j ], t, _mm256_cmpeq_epi64( idx[ j ], o ) );
+    old = old + 1u >= depth ? 0u : old + 1u;
+    res[ i ] = FD_TXN_VERIFY_SUCCESS;
+    sig[ i ] = tag;
+  }
+  for( int j=0; j<NR; j++ ) _mm256_store_si256( (__m256i *)(buf + 4*j), r[ j ] );
+  memcpy( tc->ring, buf, depth * sizeof(uint64_t) );
+  tc->oldest = old;
+  tc_map_rebuild( tc );
+}
+
+/* The tcache steps of one batch, in frag order (fd_verify.h:63-86): per
+   frag, query (DEDUP), the verify result (FAILED; signature_cnt 0 or > 16
+   folds to ERR_SIG, so FAILED too), insert (SUCCESS, opt_sig = tag).
+   ring != 0 allows the register form for small tcaches. */
+static void
+vs_tcache_steps( fd_ed25519_gpu_tcache_t * tc, int8_t * res, uint64_t const * tg, uint64_t * sig, uint64_t n,
+                 int ring ) {
+  static int const avx2 = __builtin_cpu_supports( "avx2" );
+  if( ring && avx2 && tc->depth <= 16u ) { vs_replay_ring<4>( tc, res, tg, sig, n ); return; }
+  if( ring && avx2 && tc->depth <= 32u ) { vs_replay_ring<8>( tc, res, tg, sig, n ); return; }
+  for( uint64_t i=0; i<n; i++ ) {
+    int8_t v = res[ i ];
+    uint64_t tag = tg[ i ];
+    sig[ i ] = 0u;
+    if( v == FD_TXN_VERIFY_BAD_FRAG ) continue;
+    int r = tc_query_insert( tc, tag, v == FD_ED25519_SUCCESS );
+    if( r > 0 )      res[ i ] = FD_TXN_VERIFY_DEDUP;
+    else if( r < 0 ) res[ i ] = FD_TXN_VERIFY_FAILED;
+    else           { res[ i ] = FD_TXN_VERIFY_SUCCESS; sig[ i ] = tag; }
+  }
+}
+
+/* Test hook (tests only): the tcache steps over caller arrays, in the
+   register form (ring = 1, when the tcache is small enough and the host has
+   AVX2) or the map form (0). */
+extern "C" void
+fd_ed25519_gpu_test_tcache_steps( fd_ed25519_gpu_tcache_t * tc, int8_t * res, uint64_t const * tag, uint64_t * sig,
+                                  uint64_t n, int ring, uint64_t * map_out ) {
+  vs_tcache_steps( tc, res, tag, sig, n, ring );
+  if( map_out ) memcpy( map_out, tc->map, tc->map_cnt * sizeof(uint64_t) );
 }
 
 extern "C" fd_ed25519_gpu_tcache_t *
@@ -199,6 +308,11 @@ frag_parse( uint8_t const * arena, uint64_t arena_sz, fd_ed25519_gpu_frag_t f, u
   *tag = ld64( arena + soff );
   if( moff > payload_sz ) return FD_TXN_VERIFY_BAD_FRAG;      /* msg_sz would wrap (reference reads ~2^64 B) */
   if( !cnt || cnt > 16u ) return FD_TXN_VERIFY_FAILED;        /* batch_sz==0 || >16 -> ERR_SIG, fd_ed25519_user.c */
+  /* more signatures than the frag can hold (each needs its 64 bytes and its
+     signer's 32-byte address in the payload): impossible for fd_txn_parse
+     output; BAD_FRAG here as in the device parse, whose verify grid is
+     sized by this bound (FD_FRAG_SIG_BYTES) */
+  if( cnt * 96u > sz ) return FD_TXN_VERIFY_BAD_FRAG;
   if( soff + 64u * cnt > arena_sz || aoff + 32u * cnt > arena_sz ) return FD_TXN_VERIFY_BAD_FRAG;
   if( arena_sz > 0xffffffffull ) return FD_TXN_VERIFY_BAD_FRAG;  /* descriptor offsets are u32 */
   *sig_off = (uint32_t)soff; *pub_off = (uint32_t)aoff;
@@ -465,18 +579,7 @@ vs_replay( fd_ed25519_gpu_tcache_t * tc, vs_batch * b, int threads ) {
     for( int t=0; t<nt; t++ ) th.emplace_back( vs_fold_range, b, part[t], part[t+1], k0[t] );
     for( auto & x : th ) x.join();
   }
-  for( uint64_t i=0; i<n; i++ ) {
-    int8_t v = b->result[ i ];
-    uint64_t tag = b->tag[ i ];
-    b->sig[ i ] = 0u;
-    if( v == FD_TXN_VERIFY_BAD_FRAG ) continue;
-    if( v == FD_TXN_VERIFY_FAILED ) v = FD_ED25519_ERR_SIG;   /* signature_cnt 0 or > 16 */
-    if( fd_ed25519_gpu_tcache_query( tc, tag ) ) { b->result[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
-    if( v != FD_ED25519_SUCCESS )                { b->result[ i ] = FD_TXN_VERIFY_FAILED; continue; }
-    if( tc_insert( tc, tag ) )                   { b->result[ i ] = FD_TXN_VERIFY_DEDUP;  continue; }
-    b->result[ i ] = FD_TXN_VERIFY_SUCCESS;
-    b->sig[ i ] = tag;
-  }
+  vs_tcache_steps( tc, b->result, b->tag.data(), b->sig, n, 1 );
 }
 
 static inline uint64_t vs_now( void ) {

@@ -588,6 +588,16 @@ int fd_ed25519_gpu_test_copy_plan( int kind, void const * items, uint64_t n, uin
                                    int nslot, uint64_t * bytes, uint64_t * runs,
                                    uint8_t * image, uint64_t image_cap, void * rebased );
 
+/* Test hook (not part of the reference interface): the verify stage's
+   in-order tcache steps (fd_verify.h:63-86) over n frags -- res[i] the
+   frag's verify code or FD_TXN_VERIFY_BAD_FRAG in, its FD_TXN_VERIFY_* result
+   out; sig[i] its opt_sig -- in the form the stage uses for small tcaches
+   (ring = 1: the ring in registers, the map rebuilt after the batch, when
+   depth <= 32 and the host has AVX2) or the map form (ring = 0).  map_out
+   (NULL: skip) gets the map's map_cnt slots afterwards. */
+void fd_ed25519_gpu_test_tcache_steps( fd_ed25519_gpu_tcache_t * tc, int8_t * res, uint64_t const * tag,
+                                       uint64_t * sig, uint64_t n, int ring, uint64_t * map_out );
+
 /* Test hook (not part of the reference interface): runs the device lattice
    reduction (firedancer_amd/csrc/fd_lattice_dev.h) on n scalars k (8 LE
    u32 words each, k < l) on the context's first device.  out: n records of

@@ -129,6 +129,65 @@ def test_tcache_matches_reference(ref, depth, map_cnt):
         assert tc.query(t) == (t in ref_set or t == 0), t
 
 
+@pytest.mark.parametrize("depth,map_cnt", [(16, 64), (5, 8), (1, 4), (16, 0), (30, 32), (32, 64), (100, 0)])
+def test_tcache_steps_ring_form_vs_reference(ref, depth, map_cnt):
+    """The stage's tcache steps in the register-ring form (depth <= 32: the
+    ring in AVX2 registers, the map rebuilt after each batch) against the
+    map form and the REFERENCE tcache: per-frag results, opt_sig, and the
+    final map slot for slot after every batch (colliding tags, tag 0, all
+    result kinds, batches in sequence)."""
+    import ctypes as C
+    lib = fa.load_lib()
+    vp = C.c_void_p
+    lib.fd_ed25519_gpu_test_tcache_steps.argtypes = [vp, vp, vp, vp, C.c_uint64, C.c_int, vp]
+    rng = np.random.default_rng(depth * 7 + map_cnt)
+    pool = [int(x) for x in rng.integers(1, 1 << 62, size=3 * depth + 8, dtype=np.int64)]
+    pool = [(t & ~0x7) | (i & 0x3) for i, t in enumerate(pool)] + [0, 8, 16, 24]
+    codes = np.array([0, 0, 0, 0, -4, -1, -2, BAD], np.int8)        # SUCCESS x4, ERR_MSG/SIG/PUBKEY, BAD_FRAG
+    tcs = [fa.TCache(depth, map_cnt), fa.TCache(depth, map_cnt)]
+    mc = tcs[0].map_cnt
+    ops = []
+    for batch in range(4):
+        n = int(rng.integers(1, 600))
+        tags = np.array([pool[int(i)] for i in rng.integers(0, len(pool), size=n)], np.uint64)
+        res0 = codes[rng.integers(0, len(codes), size=n)]
+        outs = []
+        for ring, tc in zip((1, 0), tcs):
+            res = res0.copy(); sig = np.zeros(n, np.uint64); mp = np.zeros(mc, np.uint64)
+            lib.fd_ed25519_gpu_test_tcache_steps(tc.tc, _vp(res), _vp(tags), _vp(sig), n, ring, _vp(mp))
+            outs.append((res, sig, mp))
+        assert all(np.array_equal(a, b) for a, b in zip(outs[0], outs[1]))
+        res, sig, mp = outs[0]
+        assert np.array_equal(sig, np.where(res == S, tags, 0).astype(np.uint64))
+        # the same steps as reference tcache ops over the whole history: a
+        # query per frag with a result, an insert after each that succeeds
+        start = len(ops)
+        for j in range(n):
+            if res0[j] == BAD:
+                continue
+            ops.append((0, int(tags[j])))
+            if res[j] == S:
+                ops.append((1, int(tags[j])))
+        o = np.array(ops, np.uint64).reshape(-1, 2)
+        out = np.zeros(len(o), np.int32)
+        mapo = np.zeros(4096, np.uint64); ringo = np.zeros(depth, np.uint64); oldest = np.zeros(1, np.uint64)
+        assert ref.fdref_tcache_seq(depth, map_cnt, _vp(o), len(o), _vp(out), _vp(mapo), _vp(ringo), _vp(oldest)) == mc
+        assert np.array_equal(mapo[:mc], mp), batch
+        k = start
+        for j in range(n):
+            if res0[j] == BAD:
+                assert res[j] == BAD
+                continue
+            found = int(out[k]); k += 1
+            if found:
+                assert res[j] == D
+            elif res0[j] == 0:
+                assert res[j] == S and int(out[k]) == 0
+                k += 1
+            else:
+                assert res[j] == F
+
+
 def test_tcache_params():
     with pytest.raises(ValueError):
         fa.TCache(0, 64)
@@ -190,18 +249,25 @@ def _corrupt_frags(arena, frags, kind, i):
     elif kind == "outside":
         frags["off"][i] = len(arena) - 4
         frags["sz"][i] = 8
+    elif kind == "overclaim":
+        # 16 signatures claimed by a frag too small to hold them (96 B each:
+        # impossible for fd_txn_parse output) -> BAD_FRAG in both parses
+        assert sz < 16 * 96
+        arena[t + 1] = 16
+
+
+BAD_KINDS = ["short", "mtu", "rbh", "nosig", "manysig", "outside", "overclaim", None]
 
 
 def test_frags_to_descs_bad_frags():
     fx = fixture_txns()
-    kinds = ["short", "mtu", "rbh", "nosig", "manysig", "outside", None]
-    arena, frags = _mk_frags([fx["valid_txn_1sig"]] * len(kinds))
-    for i, k in enumerate(kinds):
+    arena, frags = _mk_frags([fx["valid_txn_1sig"]] * len(BAD_KINDS))
+    for i, k in enumerate(BAD_KINDS):
         _corrupt_frags(arena, frags, k, i)
     desc, st, tag = fa.frags_to_descs(arena, len(arena), frags)
-    assert list(st) == [BAD, BAD, BAD, F, F, BAD, 0]
-    assert len(desc) == 1 and int(desc[0]["txn_idx"]) == 6
-    assert int(tag[3]) == int(tag[6]) != 0
+    assert list(st) == [BAD, BAD, BAD, F, F, BAD, BAD, 0]
+    assert len(desc) == 1 and int(desc[0]["txn_idx"]) == 7
+    assert int(tag[3]) == int(tag[7]) != 0
 
 
 def test_frags_reference_sanity_checks_agree(ref):
@@ -428,3 +494,25 @@ def test_offload_link_served_on_gpu_vs_reference_tile(gpu, ref):
     assert stats[1] == len(frags)
     bad = np.nonzero((got_r != exp_res) | (got_s != exp_tag))[0]
     assert len(bad) == 0, [(int(j), int(got_r[j]), int(exp_res[j])) for j in bad[:10]]
+
+
+@pytest.mark.gpu
+def test_stage_device_parse_bad_frags(gpu):
+    """The device parse classifies every sanity failure as the host parse
+    does -- including a frag claiming more signatures than it can hold,
+    which the verify grid's size relies on (FD_FRAG_SIG_BYTES)."""
+    fx = fixture_txns()
+    arena, frags = _mk_frags([fx["valid_txn_1sig"]] * len(BAD_KINDS) + [fx["valid_txn_2sigs"]])
+    for i, k in enumerate(BAD_KINDS):
+        _corrupt_frags(arena, frags, k, i)
+    out = {}
+    for devparse in (True, False):
+        ast = fa.AsyncStage(gpu, fa.TCache(), 64, threads=1, device_parse=devparse)
+        res = np.zeros(len(frags), np.int8); sig = np.zeros(len(frags), np.uint64)
+        ast.submit(arena, len(arena), np.ascontiguousarray(frags), res, sig)
+        while ast.pending():
+            ast.poll(True)
+        ast.close()
+        out[devparse] = (res.copy(), sig.copy())
+    assert list(out[True][0]) == [BAD, BAD, BAD, F, F, BAD, BAD, S, S]
+    assert np.array_equal(out[True][0], out[False][0]) and np.array_equal(out[True][1], out[False][1])
