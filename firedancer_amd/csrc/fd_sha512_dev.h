@@ -1,6 +1,7 @@
 /* fd_sha512_dev.h -- per-lane SHA-512 for gfx950: the 8x64-bit state and
-   the 16-word rolling message schedule live in VGPRs (64-bit ops lower to
-   32-bit pairs: v_add_co/v_addc, v_alignbit rotates, v_bfi for Ch/Maj).
+   the 16-word rolling message schedule live in VGPRs (64-bit adds as
+   v_lshl_add_u64, rotates as v_alignbit_b32 pairs, Ch as v_bfi_b32, Maj and
+   the three-way XORs as v_bitop3_b32).
 
    Replaces the verify-path use of fd_sha512_init/append/fini
    (src/ballet/sha512/fd_sha512.c:264-399; cores fd_sha512_core_ref :128-229
@@ -54,20 +55,50 @@ FD_SHA_FN uint64_t sha_ror( uint64_t x, int n ) {
 #endif
 }
 
-/* Ch(e,f,g) = (e & f) ^ (~e & g) = bitfield insert; Maj(a,b,c) = (a^b) ? c : b. */
-FD_SHA_FN uint64_t sha_ch ( uint64_t e, uint64_t f, uint64_t g ) { return (e & f) | (~e & g); }
+/* Ch(e,f,g) = (e & f) | (~e & g): one v_bfi_b32 per half (left to itself
+   the compiler emits an and, a bfi and an extra 64-bit add per half).
+   Maj(a,b,c) and the three-way XORs of the Sigma functions: one
+   v_bitop3_b32 per half (gfx950's three-input bitwise op, truth tables 0xE8
+   and 0x96 -- both symmetric, so the operand order does not matter) instead
+   of two or three two-input ops. */
 #if defined(__HIP_DEVICE_COMPILE__)
-/* Maj as v_bfi_b32 per half (the compiler otherwise expands it to and/or) */
 FD_SHA_FN uint32_t sha_bfi( uint32_t m, uint32_t x, uint32_t y ) {
   uint32_t r; asm( "v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y) ); return r;
 }
+FD_SHA_FN uint32_t sha_x3( uint32_t a, uint32_t b, uint32_t c ) { return __builtin_amdgcn_bitop3_b32( a, b, c, 0x96 ); }
+FD_SHA_FN uint32_t sha_mj( uint32_t a, uint32_t b, uint32_t c ) { return __builtin_amdgcn_bitop3_b32( a, b, c, 0xe8 ); }
+/* The two halves as one 64-bit register pair, opaque to the optimiser:
+   left visible, it splits the 64-bit add the pair feeds into an add of the
+   zero-extended low half and one of the high half (two adds, two moves). */
+FD_SHA_FN uint64_t sha_pair( uint32_t lo, uint32_t hi ) {
+  uint64_t r = ((uint64_t)hi << 32) | lo;
+  asm( "" : "+v"(r) );
+  return r;
+}
+/* x >> n as one v_lshrrev_b64 (split into halves the compiler makes it a
+   shift and an alignbit) */
+FD_SHA_FN uint64_t sha_shr( uint64_t x, int n ) {
+  uint64_t r = x >> n;
+  asm( "" : "+v"(r) );
+  return r;
+}
+FD_SHA_FN uint64_t sha_ch( uint64_t e, uint64_t f, uint64_t g ) {
+  return sha_pair( sha_bfi( (uint32_t)e, (uint32_t)f, (uint32_t)g ),
+                   sha_bfi( (uint32_t)(e >> 32), (uint32_t)(f >> 32), (uint32_t)(g >> 32) ) );
+}
 FD_SHA_FN uint64_t sha_maj( uint64_t a, uint64_t b, uint64_t c ) {
-  uint64_t m = a ^ b;
-  return ((uint64_t)sha_bfi( (uint32_t)(m >> 32), (uint32_t)(c >> 32), (uint32_t)(b >> 32) ) << 32) |
-         sha_bfi( (uint32_t)m, (uint32_t)c, (uint32_t)b );
+  return sha_pair( sha_mj( (uint32_t)a, (uint32_t)b, (uint32_t)c ),
+                   sha_mj( (uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32) ) );
+}
+FD_SHA_FN uint64_t sha_xor3( uint64_t a, uint64_t b, uint64_t c ) {
+  return sha_pair( sha_x3( (uint32_t)a, (uint32_t)b, (uint32_t)c ),
+                   sha_x3( (uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32) ) );
 }
 #else
-FD_SHA_FN uint64_t sha_maj( uint64_t a, uint64_t b, uint64_t c ) { uint64_t m = a ^ b; return (m & c) | (~m & b); }
+FD_SHA_FN uint64_t sha_shr ( uint64_t x, int n ) { return x >> n; }
+FD_SHA_FN uint64_t sha_ch  ( uint64_t e, uint64_t f, uint64_t g ) { return (e & f) | (~e & g); }
+FD_SHA_FN uint64_t sha_maj ( uint64_t a, uint64_t b, uint64_t c ) { return (a & b) | (a & c) | (b & c); }
+FD_SHA_FN uint64_t sha_xor3( uint64_t a, uint64_t b, uint64_t c ) { return a ^ b ^ c; }
 #endif
 
 FD_SHA_FN void sha512_init_state( uint64_t h[ 8 ] ) {
@@ -76,8 +107,8 @@ FD_SHA_FN void sha512_init_state( uint64_t h[ 8 ] ) {
 }
 
 #define SHA_ROUND( a, b, c, d, e, f, g, hh, k, w ) do {                                               \
-    uint64_t t1 = hh + (sha_ror( e, 14 ) ^ sha_ror( e, 18 ) ^ sha_ror( e, 41 )) + sha_ch( e, f, g ) + (k) + (w); \
-    uint64_t t2 = (sha_ror( a, 28 ) ^ sha_ror( a, 34 ) ^ sha_ror( a, 39 )) + sha_maj( a, b, c );           \
+    uint64_t t1 = hh + sha_xor3( sha_ror( e, 14 ), sha_ror( e, 18 ), sha_ror( e, 41 ) ) + sha_ch( e, f, g ) + (k) + (w); \
+    uint64_t t2 = sha_xor3( sha_ror( a, 28 ), sha_ror( a, 34 ), sha_ror( a, 39 ) ) + sha_maj( a, b, c );           \
     d += t1; hh = t1 + t2; } while( 0 )
 
 /* One 128-byte block, W[16] big-endian words (clobbered).  16 rounds per
@@ -91,8 +122,8 @@ FD_SHA_FN void sha512_compress( uint64_t h[ 8 ], uint64_t W[ 16 ] ) {
 #pragma unroll
       for( int i=0; i<16; i++ ) {
         uint64_t w15 = W[(i+1)&15], w2 = W[(i+14)&15];
-        uint64_t s0 = sha_ror( w15, 1 ) ^ sha_ror( w15, 8 ) ^ (w15 >> 7);
-        uint64_t s1 = sha_ror( w2, 19 ) ^ sha_ror( w2, 61 ) ^ (w2 >> 6);
+        uint64_t s0 = sha_xor3( sha_ror( w15, 1 ), sha_ror( w15, 8 ), sha_shr( w15, 7 ) );
+        uint64_t s1 = sha_xor3( sha_ror( w2, 19 ), sha_ror( w2, 61 ), sha_shr( w2, 6 ) );
         W[i] = W[i] + s0 + W[(i+9)&15] + s1;
       }
     }
