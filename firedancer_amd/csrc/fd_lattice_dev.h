@@ -235,25 +235,27 @@ FD_LT_FN int lat_lehmer( uint32_t x[ 8 ], uint32_t tx[ 4 ], uint32_t y[ 8 ], uin
   double a0 = 1.0, a1 = 0.0, b0 = 0.0, b1 = 1.0;     /* magnitudes of the 2x2 matrix */
   int j = 0;
   int go = act;
+  /* branch-free step (selects, no divergent ifs): the branchy form kept
+     every loop-carried double live in two register copies, ~20 moves a
+     step; a lane that stopped computes on with its state held */
   while( lat_any( go ) ) {
-    if( go ) {
-      double q = floor( A * lat_rcp( B ) );
-      double R = fma( -q, B, A );
-      if( R < 0.0 ) { q -= 1.0; R += B; }
-      if( R >= B )  { q += 1.0; R -= B; }
-      double EA = a0 + a1, EB = b0 + b1;
-      double nb0 = fma( q, b0, a0 ), nb1 = fma( q, b1, a1 );
-      /* exact iff q <= true quotient < q+1 for every x/2^e0, y/2^e0 in
-         their truncation intervals; keep every quantity below 2^53 */
-      int ok = (R - EA - q*EB >= 0.0) && (B - R - EA - (q + 1.0)*EB > 0.0) && (nb0 + nb1 < 67108864.0);
-      if( ok ) {
-        A = B; B = R;
-        a0 = b0; a1 = b1; b0 = nb0; b1 = nb1;
-        j++;
-        /* stop once the new remainder might be < 2^128 (or shrank too far to steer) */
-        if( R - (nb0 + nb1) < thr || R < 67108864.0 ) go = 0;
-      } else go = 0;
-    }
+    double q = floor( A * lat_rcp( B ) );
+    double R = fma( -q, B, A );
+    int lo = R < 0.0;
+    q = lo ? q - 1.0 : q; R = lo ? R + B : R;
+    int hi = R >= B;
+    q = hi ? q + 1.0 : q; R = hi ? R - B : R;
+    double EA = a0 + a1, EB = b0 + b1;
+    double nb0 = fma( q, b0, a0 ), nb1 = fma( q, b1, a1 );
+    /* exact iff q <= true quotient < q+1 for every x/2^e0, y/2^e0 in
+       their truncation intervals; keep every quantity below 2^53 */
+    int ok = go & (R - EA - q*EB >= 0.0) & (B - R - EA - (q + 1.0)*EB > 0.0) & (nb0 + nb1 < 67108864.0);
+    A  = ok ? B   : A;  B  = ok ? R   : B;
+    a0 = ok ? b0  : a0; a1 = ok ? b1  : a1;
+    b0 = ok ? nb0 : b0; b1 = ok ? nb1 : b1;
+    j += ok;
+    /* stop once the new remainder might be < 2^128 (or shrank too far to steer) */
+    go = ok & (R - (nb0 + nb1) >= thr) & (R >= 67108864.0);
   }
   if( act && j ) {
     /* (x', y') = j even: (a0 x - a1 y, b1 y - b0 x); j odd: negated */
