@@ -148,6 +148,7 @@ __device__ __forceinline__ void sha_fetch( uint32_t raw[ 33 ], uint32_t const * 
 /* SHA-512(R || A || M) mod l.  R, A: 8 LE words each; the message is
    streamed from HBM, each block's dwords fetched one block ahead so the
    load latency hides behind the previous compression. */
+template<bool FASTBLK>
 __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 ], uint32_t const Aw[ 8 ],
                                           uint8_t const * arena, uint32_t msg_off, uint32_t msg_sz, uint32_t lim_dw ) {
   uint64_t h[ 8 ]; sha512_init_state( h );
@@ -163,6 +164,25 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
     for( int i=0; i<33; i++ ) raw[i] = nxt[i];
     if( b + 1u < nblk ) sha_fetch( nxt, a32, msg_off, b + 1u, lim_dw );
     uint64_t W[ 16 ];
+    /* a block whose message bytes all lie before msg_sz on every lane of
+       the wave (every block but the last one or two) needs no padding
+       masks: the wave-uniform fast form assembles just the bytes (not in
+       the pipe kernel's phase A: its extra registers spill there) */
+    if( FASTBLK && __all( (b << 7) + 64u <= msg_sz ) ) {
+#pragma unroll
+      for( int j=0; j<16; j++ ) {
+        uint32_t hi, lo;
+        if( b == 0 && j < 8 ) {
+          uint32_t const * src = (j < 4) ? Rw : Aw;
+          int jj = j & 3;
+          hi = sha_bswap32( src[2*jj] ); lo = sha_bswap32( src[2*jj+1] );
+        } else {
+          hi = sha_bswap32( __builtin_amdgcn_alignbyte( raw[2*j+1], raw[2*j],   sh ) );
+          lo = sha_bswap32( __builtin_amdgcn_alignbyte( raw[2*j+2], raw[2*j+1], sh ) );
+        }
+        W[j] = ((uint64_t)hi << 32) | lo;
+      }
+    } else {
 #pragma unroll
     for( int j=0; j<16; j++ ) {
       uint32_t hi, lo;                                  /* big-endian halves */
@@ -188,6 +208,7 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
         if( b == nblk-1u && j == 14 ) { hi = 0u; lo = 0u; }
       }
       W[j] = ((uint64_t)hi << 32) | lo;
+    }
     }
     sha512_compress( h, W );
   }
@@ -468,6 +489,7 @@ __device__ __forceinline__ void recode_p_lds( uint8_t * row, uint32_t const x[ 8
 /* k = SHA-512(R||A||M) mod l (:203-206), the lattice vector (u, v, sign
    of u) of k (fd_lattice_dev.h) and w = v S mod l, for a live lane; *nbits =
    the longer of u, v in bits. */
+template<bool FASTBLK>
 __device__ __forceinline__ void verify_prep_scalars( uint32_t u[ 8 ], uint32_t v[ 8 ], int * un, uint32_t w[ 8 ], int * nbits,
                                                      uint32_t const sig[ 16 ], uint32_t const pub[ 8 ], verify_args const & args,
                                                      fd_ed25519_desc_t const & d, uint32_t lim_dw
@@ -476,7 +498,7 @@ __device__ __forceinline__ void verify_prep_scalars( uint32_t u[ 8 ], uint32_t v
 #endif
                                                      ) {
   uint32_t k[ 8 ];
-  hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );
+  hash_ram<FASTBLK>( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );
   FE_FENCE();
   STAMP( 2 );
   lat_short_vector( k, u, v, un );
@@ -514,7 +536,7 @@ __device__ __forceinline__ void verify_prep_digits( uint8_t * drow, uint64_t str
   for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; }
   if( live ) {
     uint32_t w[ 8 ];
-    verify_prep_scalars( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
+    verify_prep_scalars<true>( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
 #ifdef FD_PHASE_STAMPS
                          , _st
 #endif
@@ -923,7 +945,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
     int nbits = 0;
 #pragma unroll
     for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; w[j] = 0u; }
-    if( live ) verify_prep_scalars( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
+    if( live ) verify_prep_scalars<true>( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
 #ifdef FD_PHASE_STAMPS
                                     , _st
 #endif
@@ -1290,7 +1312,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
     int un = 0, nbits = 0;
 #pragma unroll
     for( int j=0; j<8; j++ ) { u[j] = 0u; v[j] = 0u; w[j] = 0u; }
-    if( live ) verify_prep_scalars( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
+    if( live ) verify_prep_scalars<false>( u, v, &un, w, &nbits, sig, pub, args, d, lim_dw
 #ifdef FD_PHASE_STAMPS
                                     , nullptr
 #endif
@@ -1764,7 +1786,7 @@ fd_ed25519_verify_cached_kernel( verify_args args ) {
   uint32_t k[ 8 ];
 #pragma unroll
   for( int j=0; j<8; j++ ) k[j] = 0u;
-  if( live ) hash_ram( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );   /* :203-206 */
+  if( live ) hash_ram<true>( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );   /* :203-206 */
   FE_FENCE();
   ge_p3 R;
   int smR;
