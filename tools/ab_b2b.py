@@ -6,6 +6,10 @@ the figure as it is in bench.py's ms_per_step.  Codes are checked after a
 flush.
 
   python3 tools/ab_b2b.py A.so B.so [C.so ...] [burst]
+
+A library argument may carry settings read when its context first launches
+the pipe (A.so@FD_ED25519_GPU_PIPE_KB=7,OTHER=1): the same build under
+different knobs, one context each.
 """
 import ctypes
 import os
@@ -19,8 +23,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402  (the bench's own synthetic workload)
 
-libs = [a for a in sys.argv[1:] if a.endswith(".so")]
-burst = int(sys.argv[-1]) if not sys.argv[-1].endswith(".so") else 20
+specs = [a for a in sys.argv[1:] if ".so" in a]
+libs = specs
+burst = int(sys.argv[-1]) if ".so" not in sys.argv[-1] else 20
 n = 65536
 arena, desc, sz, expect, _ = bench.build_workload(n, 200, seed=0, n_keys=None)
 d_arena = torch.from_numpy(arena).cuda()
@@ -30,7 +35,10 @@ st = torch.cuda.Stream()
 torch.cuda.set_stream(st)
 vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
 ctx = []
-for p in libs:
+envs = []
+for spec in libs:
+    p, _, env = spec.partition("@")
+    envs.append(dict(kv.split("=", 1) for kv in env.split(",")) if env else {})
     lib = ctypes.CDLL(os.path.abspath(p))
     lib.fd_ed25519_gpu_new.restype = vp
     lib.fd_ed25519_gpu_new.argtypes = [u64, u64]
@@ -47,6 +55,15 @@ def launch(k):
     assert r == 0, r
 
 
+for k in range(len(libs)):                 # each context's first launch under its settings
+    saved = {key: os.environ.get(key) for key in envs[k]}
+    os.environ.update(envs[k])
+    launch(k)
+    for key, v in saved.items():
+        if v is None:
+            os.environ.pop(key, None)
+        else:
+            os.environ[key] = v
 for _ in range(100):                       # clock ramp
     for k in range(len(libs)):
         launch(k)
