@@ -305,8 +305,10 @@ __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint6
 #else
 #pragma unroll
   for( int j=0; j<8; j++ ) m[j] = make_uint4( w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
+#if !defined(FD_DIAG_VTAB_NO_TAIL)   /* diagnostic (wrong results): the entry's 32-B tail never stored nor read -- the byte cut of 128-B packed entries without their packing work */
 #pragma unroll
   for( int j=0; j<2; j++ ) tl[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
+#endif
 #endif
 }
 
@@ -656,7 +658,9 @@ __device__ __forceinline__ void vtab_fetch_lds( uint4 * buf, uint32_t const * vt
   uint4 const * m; uint4 const * tl;
   vtab_ptrs( vtab, cap, t, e, &m, &tl );
   glds_record<8>( m, buf );
+#if !defined(FD_DIAG_VTAB_NO_TAIL)
   glds_record<2>( tl, buf + 64*8 );
+#endif
 }
 
 /* Comb-table entry |d| of position k into buf[8][64]. */

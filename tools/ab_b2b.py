@@ -84,7 +84,9 @@ for lib, c in ctx:
     assert lib.fd_ed25519_gpu_pipe_flush_dev(c, 0, st.cuda_stream) == 0
 torch.cuda.synchronize()
 for k, p in enumerate(libs):
-    assert np.array_equal(outs[k].cpu().numpy(), expect), p
+    # AB_NOCHECK=1: diagnostic builds whose codes are wrong by design (FD_DIAG_*)
+    if os.environ.get("AB_NOCHECK") != "1":
+        assert np.array_equal(outs[k].cpu().numpy(), expect), p
     t = sorted(times[k])
     print("%-40s b2b median %.4f ms/step (%.2f M verifies/s) min %.4f max %.4f" % (
         os.path.basename(p), statistics.median(t), n / statistics.median(t) / 1e3, t[0], t[-1]), flush=True)
