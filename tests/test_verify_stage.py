@@ -516,3 +516,37 @@ def test_stage_device_parse_bad_frags(gpu):
         out[devparse] = (res.copy(), sig.copy())
     assert list(out[True][0]) == [BAD, BAD, BAD, F, F, BAD, BAD, S, S]
     assert np.array_equal(out[True][0], out[False][0]) and np.array_equal(out[True][1], out[False][1])
+
+
+@pytest.mark.gpu
+def test_stage_device_parse_many_workgroups(gpu):
+    """One device-parsed batch of 70,000 frags: 274 parse workgroups, so the
+    last workgroup's scan of the workgroup totals runs two rounds (its loop
+    over 256 totals at a time), and frags cross every workgroup boundary.
+    The stage's results equal the host parse's, frag for frag (both replay
+    the same tcache steps over the same stream: a pool of 2,500 signed txns
+    with 1-4 signatures, some corrupted, repeated)."""
+    rng = np.random.default_rng(2024)
+    n = 70000
+    arena_u, frags_u = _random_frag_stream(rng, 2500, 2500)
+    order = rng.integers(0, len(frags_u), size=n)
+    frags = np.zeros(n, frags_u.dtype)
+    frags["off"] = frags_u["off"][order]
+    frags["sz"] = frags_u["sz"][order]
+    big = fa.Ed25519Gpu(device_mask=1, max_batch=16 * n)
+    out = {}
+    try:
+        for devparse in (True, False):
+            ast = fa.AsyncStage(big, fa.TCache(), n, threads=8, device_parse=devparse)
+            res = np.zeros(n, np.int8); sig = np.zeros(n, np.uint64)
+            ast.submit(arena_u, len(arena_u), np.ascontiguousarray(frags), res, sig)
+            while ast.pending():
+                ast.poll(True)
+            ast.close()
+            out[devparse] = (res, sig)
+    finally:
+        big.close()
+    bad = np.nonzero((out[True][0] != out[False][0]) | (out[True][1] != out[False][1]))[0]
+    assert len(bad) == 0, [(int(j), int(out[True][0][j]), int(out[False][0][j])) for j in bad[:10]]
+    hist = {int(k): int(v) for k, v in zip(*np.unique(out[True][0], return_counts=True))}
+    assert hist.get(S, 0) > 1000 and hist.get(D, 0) > 1000, hist
