@@ -519,15 +519,16 @@ def test_stage_device_parse_bad_frags(gpu):
 
 
 @pytest.mark.gpu
-def test_stage_device_parse_many_workgroups(gpu):
-    """One device-parsed batch of 70,000 frags: 274 parse workgroups, so the
-    last workgroup's scan of the workgroup totals runs two rounds (its loop
-    over 256 totals at a time), and frags cross every workgroup boundary.
-    The stage's results equal the host parse's, frag for frag (both replay
-    the same tcache steps over the same stream: a pool of 2,500 signed txns
-    with 1-4 signatures, some corrupted, repeated)."""
-    rng = np.random.default_rng(2024)
-    n = 70000
+@pytest.mark.parametrize("n", [60000, 70000])
+def test_stage_device_parse_many_workgroups(gpu, n):
+    """One device-parsed batch of 60,000 frags (235 parse workgroups, the
+    pipelined verify kernel: at most one wave per SIMD) and of 70,000 (274
+    workgroups, so the last workgroup's scan of the workgroup totals runs two
+    rounds of 256; the one-shot kernels); frags cross every workgroup
+    boundary.  The stage's results equal the host parse's, frag for frag
+    (both replay the same tcache steps over the same stream: a pool of 2,500
+    signed txns with 1-8 signatures, some corrupted, repeated)."""
+    rng = np.random.default_rng(2024 + n)
     arena_u, frags_u = _random_frag_stream(rng, 2500, 2500)
     order = rng.integers(0, len(frags_u), size=n)
     frags = np.zeros(n, frags_u.dtype)
