@@ -214,6 +214,24 @@ static void check_tcache( int iters ) {
   if( fd_ed25519_gpu_tcache_new( 0, 0 ) || fd_ed25519_gpu_tcache_new( 16, 17 ) || fd_ed25519_gpu_tcache_new( 16, 16 ) ) {
     fprintf( stderr, "bad tcache params accepted\n" ); exit( 1 );
   }
+  /* the replay's tcache steps, register-ring form against the map form, at
+     depths across the ring forms' limits (4 and 8 registers, then the map) */
+  uint64_t depths[] = { 1, 2, 15, 16, 17, 31, 32, 33 };
+  int8_t const codes[] = { 0, 0, 0, -4, -1, FD_TXN_VERIFY_BAD_FRAG };
+  for( uint64_t d : depths ) {
+    fd_ed25519_gpu_tcache_t * a = fd_ed25519_gpu_tcache_new( d, 0 ), * b = fd_ed25519_gpu_tcache_new( d, 0 );
+    uint64_t mc = fd_ed25519_gpu_tcache_map_cnt( a );
+    for( int it=0; it<iters/64 + 1; it++ ) {
+      uint64_t n = rnd( 300 );
+      std::vector<uint64_t> tag( n ), sa( n ), sb( n ), ma( mc ), mb( mc );
+      std::vector<int8_t> ra( n ), rb( n );
+      for( uint64_t i=0; i<n; i++ ) { tag[i] = rnd( 4 ) ? rnd( 3 * d + 3 ) : rng(); ra[i] = rb[i] = codes[ rnd( 6 ) ]; }
+      fd_ed25519_gpu_test_tcache_steps( a, ra.data(), tag.data(), sa.data(), n, 1, ma.data() );
+      fd_ed25519_gpu_test_tcache_steps( b, rb.data(), tag.data(), sb.data(), n, 0, mb.data() );
+      if( ra != rb || sa != sb || ma != mb ) { fprintf( stderr, "tcache steps: ring and map forms differ (depth %lu)\n", (unsigned long)d ); exit( 1 ); }
+    }
+    fd_ed25519_gpu_tcache_delete( a ); fd_ed25519_gpu_tcache_delete( b );
+  }
 }
 
 static void check_precompile( int iters ) {
