@@ -286,7 +286,7 @@ def hostfed_main(args):
         # async pipelined stream of 64K batches, QUEUE_DEPTH in flight
         bs = 65536
         parts = [(i, min(bs, n - i)) for i in range(0, n, bs)]
-        reps = max(1, 16 * bs // n)
+        reps = max(4, 64 * bs // n)          # 64 batches at config 2, 64 chunks at config 3: fill and drain < 5 %
 
         def stream():
             outs = [np.zeros(c, np.int8) for _, c in parts] * reps
