@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--async-batch", type=int, default=32768)
+    ap.add_argument("--async-batch", type=int, default=35000)
     args = ap.parse_args()
     import firedancer_amd as fa
 
