@@ -535,14 +535,19 @@ def test_stage_device_parse_many_workgroups(gpu, n):
     frags["off"] = frags_u["off"][order]
     frags["sz"] = frags_u["sz"][order]
     big = fa.Ed25519Gpu(device_mask=1, max_batch=16 * n)
-    out = {}
+    out, stats = {}, {}
     try:
         for devparse in (True, False):
+            if devparse:
+                big.host_stats(reset=True)
             ast = fa.AsyncStage(big, fa.TCache(), n, threads=8, device_parse=devparse)
             res = np.zeros(n, np.int8); sig = np.zeros(n, np.uint64)
             ast.submit(arena_u, len(arena_u), np.ascontiguousarray(frags), res, sig)
             while ast.pending():
                 ast.poll(True)
+            stats[devparse] = ast.stats()
+            if devparse:
+                hs = big.host_stats()
             ast.close()
             out[devparse] = (res, sig)
     finally:
@@ -550,4 +555,7 @@ def test_stage_device_parse_many_workgroups(gpu, n):
     bad = np.nonzero((out[True][0] != out[False][0]) | (out[True][1] != out[False][1]))[0]
     assert len(bad) == 0, [(int(j), int(out[True][0][j]), int(out[False][0][j])) for j in bad[:10]]
     hist = {int(k): int(v) for k, v in zip(*np.unique(out[True][0], return_counts=True))}
+    st = stats[True]
+    assert st["batches"] == 1 and st["replay_ns"] > 0, st          # the stage's own counters
+    assert hs["h2d_bytes"] >= len(arena_u) // 2, hs                 # the device parse sent the frags' pages
     assert hist.get(S, 0) > 1000 and hist.get(D, 0) > 1000, hist
