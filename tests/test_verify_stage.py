@@ -254,6 +254,10 @@ def _corrupt_frags(arena, frags, kind, i):
         # impossible for fd_txn_parse output) -> BAD_FRAG in both parses
         assert sz < 16 * 96
         arena[t + 1] = 16
+    elif kind == "claim_at_bound":
+        arena[t + 1] = sz // 96          # exactly what sz allows: parsed, verified (and failing)
+    elif kind == "claim_past_bound":
+        arena[t + 1] = sz // 96 + 1      # one more than sz allows: BAD_FRAG
 
 
 BAD_KINDS = ["short", "mtu", "rbh", "nosig", "manysig", "outside", "overclaim", None]
@@ -516,6 +520,35 @@ def test_stage_device_parse_bad_frags(gpu):
         out[devparse] = (res.copy(), sig.copy())
     assert list(out[True][0]) == [BAD, BAD, BAD, F, F, BAD, BAD, S, S]
     assert np.array_equal(out[True][0], out[False][0]) and np.array_equal(out[True][1], out[False][1])
+
+
+@pytest.mark.gpu
+def test_stage_device_parse_signature_bound_edges(gpu):
+    """The sz / 96 signature bound at its edge, device parse against host
+    parse: a frag claiming exactly sz // 96 signatures is parsed and verified
+    (its extra signatures are garbage, so it fails -- FAILED, or BAD_FRAG in
+    both if the claimed signatures run past the frag span); one more is
+    BAD_FRAG in both."""
+    fx = fixture_txns()
+    txns = [fx["valid_txn_1sig"], fx["valid_txn_2sigs"]] * 3
+    kinds = ["claim_at_bound", "claim_past_bound", None] * 2
+    arena, frags = _mk_frags(txns)
+    for i, k in enumerate(kinds):
+        _corrupt_frags(arena, frags, k, i)
+    out = {}
+    for devparse in (True, False):
+        ast = fa.AsyncStage(gpu, fa.TCache(), 64, threads=1, device_parse=devparse)
+        res = np.zeros(len(frags), np.int8); sig = np.zeros(len(frags), np.uint64)
+        ast.submit(arena, len(arena), np.ascontiguousarray(frags), res, sig)
+        while ast.pending():
+            ast.poll(True)
+        ast.close()
+        out[devparse] = (res.copy(), sig.copy())
+    assert np.array_equal(out[True][0], out[False][0]) and np.array_equal(out[True][1], out[False][1])
+    r = out[True][0]
+    assert r[1] == BAD and r[4] == BAD                     # past the bound
+    assert r[0] in (F, BAD) and r[3] in (F, BAD)           # at the bound: parsed, fails
+    assert r[2] == S and r[5] == S
 
 
 @pytest.mark.gpu
