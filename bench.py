@@ -142,25 +142,6 @@ def pmc_traffic(n, kernel, code):
     return None, "no committed PMC profile of code object %s (%s, batch %d)" % (code, kernel, n)
 
 
-def pmc_issue(n, kernel, code):
-    """The committed SQ/GRBM profile of THIS build's verify kernel (profiles/rNN/
-    pmc_sq.json, same code-object hash): VALU instructions per 64 signatures and
-    the effective clock the profiled launches ran at (GRBM_GUI_ACTIVE / 8 / t).
-    Returns (dict or None, the file used or why none was)."""
-    for r in profile_rounds():
-        path = os.path.join(REPO, "profiles", r, "pmc_sq.json")
-        if not os.path.exists(path):
-            continue
-        d = json.load(open(path))
-        if d.get("kernel") != kernel or int(d.get("grid", 0)) != 3 * n:
-            continue
-        if (d.get("build") or {}).get("code") != code:
-            continue
-        return {"valu_instr_per_64_sigs": d.get("valu_instr_per_64_sigs"),
-                "effective_clock_ghz": d.get("effective_clock_ghz")}, "profiles/%s/pmc_sq.json" % r
-    return None, "no committed SQ profile of code object %s (%s, batch %d)" % (code, kernel, n)
-
-
 def cpu_baseline(arena, desc, expect, budget_s=10.0):
     """Reference fd_ed25519_verify on this host (oracle/_ref), bounded sample:
     one pinned thread per physical core this process may use (BASELINE.md /
@@ -417,6 +398,12 @@ def launch_ranks(args):
 
 
 def main():
+    if os.environ.get("FD_MAPS_OUT"):
+        # diagnostic: the process's mappings as Python exits (the C libraries'
+        # finalizers run after this), to resolve the addresses of a crash at exit
+        import atexit
+        import shutil
+        atexit.register(shutil.copyfile, "/proc/self/maps", os.environ["FD_MAPS_OUT"])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # ~40 ms of untimed launches first: the timed region then sees the clock the
@@ -644,18 +631,6 @@ def main():
             gbs = t / (dt_max / args.steps) / 1e9
             line["roofline_hbm"] = {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
                                     "frac": gbs / 8000.0, "traffic": t}
-        # The same work priced at the clock the chip held in this build's profiled
-        # launches (it lowers its clock under this load, MI355X_MICROARCH.md "DVFS
-        # give-back"): how close the kernel's cycles come to the MAC issue rate.  A
-        # diagnostic beside `frac`, which stays priced at the nominal 2.4 GHz.
-        issue, issue_src = pmc_issue(n, kname, build.get("code")) if (pipe and args.config == 2) else (None, "config 2 pipe only")
-        if issue and issue.get("effective_clock_ghz"):
-            f = issue["effective_clock_ghz"]
-            line["roofline"]["at_profiled_clock"] = {
-                "clock_ghz": f, "peak": peak / 1e12 * f / NOMINAL_GHZ,
-                "frac": achieved / (peak * f / NOMINAL_GHZ),
-                "valu_instr_per_64_sigs": issue.get("valu_instr_per_64_sigs"), "source": issue_src,
-                "note": "clock from the profiled launches of this build (GRBM_GUI_ACTIVE/8/t), not this run"}
         if args.config != 2:   # the roofline numerator W is defined for valid 200-B verifies only
             line["roofline"]["frac_note"] = "W-based numerator is for valid 200-B verifies (config 2)"
         if world == 1 and not args.no_cpu:

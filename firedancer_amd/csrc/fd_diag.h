@@ -1,0 +1,120 @@
+/* fd_diag.h -- the wrong-results diagnostic variants of the verify kernels
+   and the host, in one place.  Each FD_DIAG_* switch builds a variant whose
+   codes are WRONG BY DESIGN (or whose ordering is deliberately broken) to
+   measure one thing -- an upper bound, a cache policy -- in a same-process
+   A/B (tools/build_var.sh, tools/ab_b2b.py with AB_NOCHECK=1; results in
+   DESIGN.md §8 / §9 and HISTORY.md).  The product sources reach them only
+   through the hooks below, which are empty unless FD_DIAG_BUILD is defined;
+   a product build (firedancer_amd/Makefile without EXTRA_DEFS) that defines
+   any FD_DIAG_* switch fails here.
+
+   Switches (FD_DIAG_BUILD required):
+     FD_DIAG_NO_VTAB_STORE   table stores skipped, the math kept
+     FD_DIAG_VTAB_ONE_ENTRY  every chain fetch reads row 0
+     FD_DIAG_VTAB_NO_TAIL    the entries' 32-B tails never stored nor read
+     FD_DIAG_SC_TABLES       table stores at system scope (sc0 sc1)
+     FD_DIAG_NT_TABLES       table stores nontemporal (correct, slower)
+     FD_DIAG_NT_INV=1|2|3    vector L1 / L2 / both invalidated at phase B/C start
+     FD_DIAG_SC_INV_AFTER    L2 invalidated once phase B's tables are stored
+     FD_DIAG_COMB_POS=k      only k comb additions
+     FD_DIAG_LSORT_TIMEOUT   every phase-A length-order wait expires
+     FD_DIAG_PIPE_OVERLAP    (host) no cross-stream order on the table scratch */
+
+#ifndef FD_DIAG_H
+#define FD_DIAG_H
+
+#if !defined(FD_DIAG_BUILD)
+#if defined(FD_DIAG_NO_VTAB_STORE) || defined(FD_DIAG_VTAB_ONE_ENTRY) || defined(FD_DIAG_VTAB_NO_TAIL) || \
+    defined(FD_DIAG_SC_TABLES) || defined(FD_DIAG_NT_TABLES) || defined(FD_DIAG_NT_INV) ||                 \
+    defined(FD_DIAG_SC_INV_AFTER) || defined(FD_DIAG_COMB_POS) || defined(FD_DIAG_LSORT_TIMEOUT) ||         \
+    defined(FD_DIAG_PIPE_OVERLAP)
+#error "FD_DIAG_* builds a wrong-results diagnostic variant: only tools/build_var.sh (FD_DIAG_BUILD) may define one"
+#endif
+#endif
+
+/* ---- product defaults (every hook empty) ---- */
+
+#define FD_VTAB_TAIL        1                 /* entries carry their 32-B tail record */
+#define FD_COMB_POS_RUN     FD_CTAB_POS       /* comb additions run by comb_lds       */
+#define FD_LSORT_SPIN       (1u << 20)        /* phase-A length-order wait bound      */
+#define FD_DIAG_VTAB_STORE( m, tl, w )   do {} while( 0 )   /* may store and return */
+#define FD_DIAG_FETCH_ENTRY( e )         do {} while( 0 )
+#define FD_DIAG_PHASE_BC_ENTRY()         do {} while( 0 )
+#define FD_DIAG_AFTER_TABLES()           do {} while( 0 )
+#define FD_DIAG_SCR_ORDER                1                 /* host: cross-stream wait on the scratch */
+
+#if defined(FD_DIAG_BUILD)
+
+#if defined(FD_DIAG_VTAB_NO_TAIL)
+#undef  FD_VTAB_TAIL
+#define FD_VTAB_TAIL 0
+#endif
+
+#if defined(FD_DIAG_COMB_POS)
+#undef  FD_COMB_POS_RUN
+#define FD_COMB_POS_RUN FD_DIAG_COMB_POS
+#endif
+
+#if defined(FD_DIAG_LSORT_TIMEOUT)
+#undef  FD_LSORT_SPIN
+#define FD_LSORT_SPIN 0u
+#endif
+
+#if defined(FD_DIAG_PIPE_OVERLAP)
+#undef  FD_DIAG_SCR_ORDER
+#define FD_DIAG_SCR_ORDER 0
+#endif
+
+#if defined(FD_DIAG_VTAB_ONE_ENTRY)
+#undef  FD_DIAG_FETCH_ENTRY
+#define FD_DIAG_FETCH_ENTRY( e ) do { (e) = 0u; } while( 0 )
+#endif
+
+#if defined(FD_DIAG_NO_VTAB_STORE)
+#undef  FD_DIAG_VTAB_STORE
+#define FD_DIAG_VTAB_STORE( m, tl, w ) do {                                                       \
+    if( (w)[0] == 0xdeadbeefu && (w)[1] == 0xdeadbeefu ) (m)[0] = make_uint4( (w)[2], (w)[3], (w)[4], (w)[5] ); \
+    return; } while( 0 )
+#elif defined(FD_DIAG_SC_TABLES)
+#undef  FD_DIAG_VTAB_STORE
+#define FD_DIAG_VTAB_STORE( m, tl, w ) do {                                                       \
+    typedef unsigned int u32x4 __attribute__(( ext_vector_type( 4 ) ));                           \
+    for( int j=0; j<8; j++ ) {                                                                    \
+      u32x4 v = { (w)[4*j], (w)[4*j+1], (w)[4*j+2], (w)[4*j+3] };                                 \
+      asm volatile( "global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"((uint64_t)((m) + j)), "v"(v) : "memory" ); \
+    }                                                                                             \
+    for( int j=0; j<2; j++ ) {                                                                    \
+      u32x4 v = { (w)[32+4*j], (w)[33+4*j], (w)[34+4*j], (w)[35+4*j] };                           \
+      asm volatile( "global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"((uint64_t)((tl) + j)), "v"(v) : "memory" ); \
+    }                                                                                             \
+    return; } while( 0 )
+#elif defined(FD_DIAG_NT_TABLES)
+#undef  FD_DIAG_VTAB_STORE
+#define FD_DIAG_VTAB_STORE( m, tl, w ) do {                                                       \
+    typedef unsigned int u32x4 __attribute__(( ext_vector_type( 4 ) ));                           \
+    for( int j=0; j<8; j++ ) { u32x4 v = { (w)[4*j], (w)[4*j+1], (w)[4*j+2], (w)[4*j+3] };        \
+      __builtin_nontemporal_store( v, (u32x4 *)(m) + j ); }                                       \
+    for( int j=0; j<2; j++ ) { u32x4 v = { (w)[32+4*j], (w)[33+4*j], (w)[34+4*j], (w)[35+4*j] };  \
+      __builtin_nontemporal_store( v, (u32x4 *)(tl) + j ); }                                      \
+    return; } while( 0 )
+#endif
+
+#if defined(FD_DIAG_NT_INV)
+#undef  FD_DIAG_PHASE_BC_ENTRY
+#if FD_DIAG_NT_INV == 1
+#define FD_DIAG_PHASE_BC_ENTRY() asm volatile( "buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory" )
+#elif FD_DIAG_NT_INV == 2
+#define FD_DIAG_PHASE_BC_ENTRY() asm volatile( "buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" )
+#else
+#define FD_DIAG_PHASE_BC_ENTRY() asm volatile( "buffer_inv sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" )
+#endif
+#endif
+
+#if defined(FD_DIAG_SC_INV_AFTER)
+#undef  FD_DIAG_AFTER_TABLES
+#define FD_DIAG_AFTER_TABLES() asm volatile( "s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" )
+#endif
+
+#endif /* FD_DIAG_BUILD */
+
+#endif /* FD_DIAG_H */

@@ -86,13 +86,18 @@ struct verify_args {
    and from phase B to phase C (2 sets): the partial sum [FD_PACC_WORDS][sig_cap]
    and the code of the checks per slot.  The arena and descriptors are read by
    phase A only. */
+/* A frag's result in the page-locked staging of the device frag path: one
+   16-byte record, written by the device with one store. */
+typedef struct __attribute__(( aligned( 16 ) )) { uint32_t tag_lo, tag_hi; int32_t status; uint32_t pad; } fd_frec_t;
+
 #define FD_PH_R           0            /* R's encoding, 8 words                        */
 #define FD_PH_YU          8            /* u + 8 (16^0 + ... + 16^(nw-2)), 8 words      */
 #define FD_PH_YV          16           /* v + the same bias, 8 words                   */
 #define FD_PH_YW          24           /* comb_bias(w) = w + 2^22 (2^0 + 2^23 + ... + 2^207)   */
 #define FD_PH_A           32           /* A's encoding, 8 words                        */
 #define FD_PH_IDX         40           /* the descriptor index the slot verifies        */
-#define FD_PH_WORDS       41
+#define FD_PH_FRAG        41           /* frag batches: frag (txn_idx) | (index in the frag) << 16 */
+#define FD_PH_WORDS       42
 #define FD_PACC_WORDS     40           /* X, Y, Z, T                                   */
 #define FD_PIPE_SETS      3
 struct pipe_args {
@@ -121,7 +126,24 @@ struct pipe_args {
   uint32_t *                err;        /* host-mapped error ring (FD_PIPE_ERR_RING words): a phase-A wait that
                                            expires stores seq + 1 at err[seq % FD_PIPE_ERR_RING] */
   uint64_t                  seq;        /* the pipe counter of the batch in phase A (its codes are the ones at risk) */
+  /* frag batches (verify stage): phase A keeps each descriptor's frag and
+     its place in the frag in the hand-off (FD_PH_FRAG: frag | k << 16);
+     phase C folds the codes per frag as it writes them (FD_FOLD_SH) with
+     fd_ed25519_verify_batch_single_msg's precedence -- first phase-1 error
+     by index, else ERR_MSG, else SUCCESS -- and the frag's last descriptor
+     to finish writes the frag's record straight to the host */
+  uint32_t const *          first_a;    /* phase A's batch is a frag batch: its frags' first descriptor indices */
+  uint64_t *                fold_c;     /* phase C's batch's fold words (FD_FOLD_*; NULL: not a frag batch) */
+  uint64_t const *          ftag_c;     /* its frags' tags */
+  fd_frec_t *               frec_c;     /* its page-locked staging records (device-mapped) */
 };
+/* A frag's fold word (64 bits, set to its descriptor count by the parse):
+   each descriptor k < 16 of the frag adds, in ONE relaxed atomic, its code
+   class << (FD_FOLD_SH + 3 k) minus 1, so the low byte counts down and the
+   descriptor fields fill in; the add that takes the count to 0 holds the
+   whole word and writes the frag's {tag, status} record to the host.
+   Classes: 0 SUCCESS, 1 ERR_MSG, 2 ERR_SIG, 3 ERR_PUBKEY, 4 BAD_DESC. */
+#define FD_FOLD_SH        8
 #define FD_PIPE_ERR_RING  64
 
 struct kpart_args {
@@ -141,30 +163,36 @@ struct kpart_args {
 };
 
 /* Device-side frag parsing (verify stage, fd_verify_stage.cpp): the frags
-   [off, off+sz) index a copy of the arena span [span_lo, span_lo+span_sz). */
+   [off, off+sz) index a copy of the arena span [span_lo, span_lo+span_sz).
+   One launch parses every frag and writes its descriptors at their final
+   positions (a single-pass scan of the per-frag signature counts with
+   decoupled look-back across workgroups, flag words tagged with the batch's
+   epoch so they need no reset). */
 struct fparse_args {
   uint8_t const *                span;       /* device copy of arena[span_lo, span_lo + span_sz) */
   uint64_t                       span_sz;
   uint64_t                       span_lo;
   uint32_t                       host_parity; /* (uintptr_t)host_arena & 1: the tile aligns host addresses */
+  uint32_t                       epoch;      /* this batch's look-back epoch (nonzero, new per batch of the slot) */
   uint64_t                       arena_sz;   /* the host arena's size (frags beyond it are BAD) */
   fd_ed25519_gpu_frag_t const *  frag;
   uint64_t                       n;
-  int8_t *                       status;     /* out: 0 / FD_TXN_VERIFY_FAILED / _BAD_FRAG, then the fold */
+  int8_t *                       status;     /* out: 0 / FD_TXN_VERIFY_FAILED / _BAD_FRAG; 0s become the folded code */
   uint64_t *                     tag;        /* out */
-  uint32_t *                     cnt;        /* out: first descriptor index, workgroup-relative */
-  uint32_t *                     fld;        /* out: 4 per frag: sig, pub, msg offsets (span-relative), msg_sz */
-  uint32_t *                     bpre;       /* out: per workgroup, its first descriptor index */
-  uint32_t *                     done;       /* workgroups finished (0 between launches) */
+  uint32_t *                     first;      /* out: the frag's first descriptor index */
+  uint64_t *                     fold;       /* out: the fold word (FD_FOLD_SH), set to the descriptor count */
+  uint64_t *                     flag;       /* look-back words, one per workgroup (zeroed once at allocation) */
   uint32_t *                     total;      /* out: descriptor count */
-  fd_ed25519_desc_t *            desc;       /* emit: descriptors */
+  uint32_t *                     err;        /* host-mapped: 1 if a look-back wait expired (the batch fails) */
+  fd_ed25519_desc_t *            desc;       /* out: descriptors */
   uint64_t                       desc_cap;
-  int8_t const *                 code;       /* fold: per-descriptor codes */
-  int8_t *                       hstatus;    /* fold: page-locked host staging (device-mapped) */
-  uint64_t *                     htag;
+  int8_t const *                 code;       /* fold kernel (one-shot verify): per-descriptor codes */
+  fd_frec_t *                    hrec;       /* page-locked host staging, one {tag lo, tag hi, status, 0} per frag
+                                                (device-mapped): the parse writes frags without descriptors, the
+                                                pipelined kernel's phase C or the fold kernel the others */
 };
 
-/* Frags per workgroup of the parse / emit / fold kernels. */
+/* Frags per workgroup of the parse and fold kernels. */
 #define FD_FRAG_BLOCK 256u
 /* Bytes of frag per signature at least: each signature's 64 bytes and its
    signer's 32-byte address lie in the frag's payload (fd_txn_parse output),
@@ -205,7 +233,6 @@ struct shred_root_args {
 #define FD_KERN_KPART    "fd_ed25519_kcache_part_kernel"
 #define FD_KERN_CACHED   "fd_ed25519_verify_cached_kernel"
 #define FD_KERN_FPARSE   "fd_frag_parse_kernel"
-#define FD_KERN_FEMIT    "fd_frag_emit_kernel"
 #define FD_KERN_FFOLD    "fd_frag_fold_kernel"
 #define FD_KERN_PIPE     "fd_ed25519_verify_pipe_kernel"
 #define FD_KERN_SHA256   "fd_sha256_batch_kernel"

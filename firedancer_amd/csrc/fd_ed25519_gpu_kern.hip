@@ -24,6 +24,7 @@
 #include "fd_sha256_dev.h"
 #include "fd_scalar_dev.h"
 #include "fd_lattice_dev.h"
+#include "fd_diag.h"
 
 /* Round-4 instruction cuts, each a build switch for same-process A/Bs
    (tools/ab_b2b.py; -DFD_OPT_X=0 builds the previous form):
@@ -31,9 +32,12 @@
                (ge_from_cached) instead of adding it to the identity;
      COMBCHK   the last comb addition folded into the final compare
                (comb_lds_eq);
-     IDROW     row 0 of every variable-base table pre-filled with the
+     IDROW     1: row 0 of every variable-base table pre-filled with the
                identity (fd_vtab_id_fill at allocation) instead of a shared
-               record selected per fetch. */
+               record selected per fetch (0); 2 (round 5): a zero digit
+               reads row 0 of table 0 through one min in the index, so every
+               zero digit of the chip hits the same two L2-resident lines
+               (1 fetched each signature's own row 0: +8.6 % HBM bytes). */
 #ifndef FD_OPT_FIRSTWIN
 #define FD_OPT_FIRSTWIN 1
 #endif
@@ -41,7 +45,15 @@
 #define FD_OPT_COMBCHK 1
 #endif
 #ifndef FD_OPT_IDROW
-#define FD_OPT_IDROW 1
+#define FD_OPT_IDROW 2
+#endif
+/*   TAIL1     (round 5, with IDROW 2) entry 1 is -Q with Q affine, so its 2Z
+               is 2 and its 32-B tail (2Z's limbs 2..9) is zero like the
+               identity row's: a digit of magnitude <= 1 reads the tail of
+               row 0 of table 0 (L2-resident), and entry 1's tail is never
+               stored. */
+#ifndef FD_OPT_TAIL1
+#define FD_OPT_TAIL1 1
 #endif
 
 /* Diagnostic build only (-DFD_PHASE_STAMPS, tools/Makefile): s_memtime at
@@ -49,7 +61,8 @@
    build compiles none of it. */
 #ifdef FD_PHASE_STAMPS
 #define FD_NSTAMP 8
-#define FD_TL_BASE 8      /* pipe-kernel timeline: 4 u64 per wave after the sums */
+#define FD_TL_BASE 8      /* pipe-kernel timeline: 4 u64 per wave after the sums (single-lane kernel: 2 per wave) */
+#define FD_STAMP_WORDS_DEV (8u + 4096u * 12u * 4u)   /* = the host's FD_STAMP_WORDS */
 #define STAMP( i ) do { FE_FENCE(); if( _st ) _st[ i ] = __builtin_amdgcn_s_memtime(); FE_FENCE(); } while( 0 )
 #else
 #define STAMP( i ) do {} while( 0 )
@@ -226,13 +239,26 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
    applied at the use point (vtab_finish).  (Storing both signs instead --
    twice the table writes for no selects at the 66 uses -- measured 8 %
    slower: the kernel runs power-limited, and the table traffic costs clock;
-   DESIGN.md §4.)  FD_DIAG_NO_VTAB_STORE / FD_DIAG_VTAB_ONE_ENTRY build the
-   diagnostic variants of those measurements (wrong results by design). */
+   DESIGN.md §4.)  The diagnostic variants of those measurements (wrong
+   results by design) hook in through fd_diag.h. */
 __device__ __forceinline__ void vtab_ptrs( uint32_t const * vtab, uint64_t cap, uint64_t t, uint32_t e,
                                            uint4 const ** m, uint4 const ** tl ) {
-  uint64_t idx = (uint64_t)e * cap + t;
+#if FD_OPT_IDROW == 2
+  /* digit 0 -> row 0 of table 0 (every row 0 is the identity): one min
+     (e << 28 exceeds e cap + t for e >= 1, as cap < 2^26 -- host-checked),
+     so all zero digits of the chip read the same two L2-hot lines */
+  uint32_t i32 = min( (uint32_t)e * (uint32_t)cap + (uint32_t)t, e << 28 );
+  uint64_t idx = i32;
+#if FD_OPT_TAIL1
+  uint64_t tdx = min( i32, (e << 28) - (1u << 28) );   /* e <= 1: 0; e >= 2: (e-1) 2^28 > e cap + t */
+#else
+  uint64_t tdx = idx;
+#endif
+#else
+  uint64_t idx = (uint64_t)e * cap + t, tdx = idx;
+#endif
   *m  = (uint4 const *)(vtab + idx * 32u);
-  *tl = (uint4 const *)(vtab + (uint64_t)FD_VTAB_N * cap * 32u + idx * 8u);
+  *tl = (uint4 const *)(vtab + (uint64_t)FD_VTAB_N * cap * 32u + tdx * 8u);
 #if !FD_OPT_IDROW
   if( !e ) {   /* the identity: one shared record after both regions (written by the host) */
     uint32_t const * id = vtab + (uint64_t)FD_VTAB_N * cap * 40u;
@@ -271,7 +297,8 @@ __device__ __forceinline__ uint32_t vtab_entry( uint32_t db ) {
   return min( e, 8u );
 }
 
-__device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint64_t t, int e, ge_cached const & c ) {
+__device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint64_t t, int e, ge_cached const & c,
+                                            bool tail = true ) {
   uint32_t w[ 40 ];
 #pragma unroll
   for( int j=0; j<10; j++ ) {
@@ -280,35 +307,14 @@ __device__ __forceinline__ void vtab_store( uint32_t * vtab, uint64_t cap, uint6
   uint4 const * mc; uint4 const * tc;
   vtab_ptrs( vtab, cap, t, (uint32_t)e, &mc, &tc );
   uint4 * m = (uint4 *)mc; uint4 * tl = (uint4 *)tc;
-#if defined(FD_DIAG_NO_VTAB_STORE)     /* diagnostic (wrong results): the stores skipped, the math kept */
-  if( w[0] == 0xdeadbeefu && w[1] == 0xdeadbeefu ) m[0] = make_uint4( w[2], w[3], w[4], w[5] );
-  return;
-#endif
-#if defined(FD_DIAG_SC_TABLES)   /* diagnostic: the table stores at system scope (sc0 sc1) */
-  typedef unsigned int u32x4 __attribute__(( ext_vector_type( 4 ) ));
-#pragma unroll
-  for( int j=0; j<8; j++ ) {
-    u32x4 v = { w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] };
-    asm volatile( "global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"((uint64_t)(m + j)), "v"(v) : "memory" );
-  }
-#pragma unroll
-  for( int j=0; j<2; j++ ) {
-    u32x4 v = { w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] };
-    asm volatile( "global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"((uint64_t)(tl + j)), "v"(v) : "memory" );
-  }
-#elif defined(FD_DIAG_NT_TABLES)   /* diagnostic: the table stores nontemporal */
-  typedef unsigned int u32x4 __attribute__(( ext_vector_type( 4 ) ));
-#pragma unroll
-  for( int j=0; j<8; j++ ) { u32x4 v = { w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] }; __builtin_nontemporal_store( v, (u32x4 *)m + j ); }
-#pragma unroll
-  for( int j=0; j<2; j++ ) { u32x4 v = { w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] }; __builtin_nontemporal_store( v, (u32x4 *)tl + j ); }
-#else
+  FD_DIAG_VTAB_STORE( m, tl, w );
 #pragma unroll
   for( int j=0; j<8; j++ ) m[j] = make_uint4( w[4*j], w[4*j+1], w[4*j+2], w[4*j+3] );
-#if !defined(FD_DIAG_VTAB_NO_TAIL)   /* diagnostic (wrong results): the entry's 32-B tail never stored nor read -- the byte cut of 128-B packed entries without their packing work */
+#if FD_VTAB_TAIL
+  if( tail ) {
 #pragma unroll
-  for( int j=0; j<2; j++ ) tl[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
-#endif
+    for( int j=0; j<2; j++ ) tl[j] = make_uint4( w[32+4*j], w[33+4*j], w[34+4*j], w[35+4*j] );
+  }
 #endif
 }
 
@@ -319,7 +325,7 @@ __device__ __forceinline__ void vtab_build( uint32_t * vtab, uint64_t cap, uint6
   ge_p3 nQ = Q;
   { fe x; fe_neg( x, Q.X ); fe_carry( nQ.X, x ); fe_neg( x, Q.T ); fe_carry( nQ.T, x ); }
   ge_cached c;
-  ge_to_cached( c, nQ );  vtab_store( vtab, cap, t, 1, c );   /* d = 0: the shared identity record */
+  ge_to_cached( c, nQ );  vtab_store( vtab, cap, t, 1, c, !(FD_OPT_IDROW == 2 && FD_OPT_TAIL1) );   /* tail: 2Z = 2, read from row 0 */
   /* -Q's affine form for the mixed additions is the cached entry without 2Z:
      Y+X and Y-X uncarried (M: ge_madd takes them only as second operands of
      fe_mul), 2dT the same product */
@@ -652,13 +658,11 @@ __device__ __forceinline__ void glds_record( void const * g, uint4 * buf ) { gld
    buf[10][64] by LDS-DMA. */
 __device__ __forceinline__ void vtab_fetch_lds( uint4 * buf, uint32_t const * vtab, uint64_t cap, uint64_t t, uint32_t db ) {
   uint32_t e = vtab_entry( db );
-#ifdef FD_DIAG_VTAB_ONE_ENTRY   /* diagnostic (wrong results): every fetch reads the shared identity record */
-  e = 0u;
-#endif
+  FD_DIAG_FETCH_ENTRY( e );
   uint4 const * m; uint4 const * tl;
   vtab_ptrs( vtab, cap, t, e, &m, &tl );
   glds_record<8>( m, buf );
-#if !defined(FD_DIAG_VTAB_NO_TAIL)
+#if FD_VTAB_TAIL
   glds_record<2>( tl, buf + 64*8 );
 #endif
 }
@@ -806,31 +810,27 @@ __device__ __forceinline__ void chain_seg( ge_p3 & acc, uint4 * buf, uint32_t co
   }
 }
 
-/* acc += [w]B: the 11 comb-table additions, w's biased digits in yw.
-   (FD_DIAG_COMB_POS < FD_CTAB_POS: diagnostic build, wrong results, timing
-   of fewer comb additions.) */
-#ifndef FD_DIAG_COMB_POS
-#define FD_DIAG_COMB_POS FD_CTAB_POS
-#endif
+/* acc += [w]B: the 11 comb-table additions, w's biased digits in yw
+   (FD_COMB_POS_RUN: fd_diag.h). */
 __device__ __forceinline__ void comb_lds( ge_p3 & acc, uint4 * buf, uint32_t const * yw, int lane, uint32_t const * ctab ) {
 #define FD_WDIG( k ) comb_digit_w( yw[ ((23*(k)) >> 5)*64 + lane ], ((23*(k)) >> 5) < 7 ? yw[ (((23*(k)) >> 5) + 1)*64 + lane ] : 0u, (k) )
   int d = FD_WDIG( 0 );
   ctab_fetch_lds( buf, ctab, 0, d );
 #pragma unroll 1
-  for( int k=0; k<FD_DIAG_COMB_POS; k++ ) {
+  for( int k=0; k<FD_COMB_POS_RUN; k++ ) {
     ge_precomp bp;
     {
       dma_wait();
       uint32_t w[ 32 ];
       lds_words<8>( w, buf, lane );
-      int dn = k + 1 < FD_DIAG_COMB_POS ? FD_WDIG( k + 1 ) : 0;
+      int dn = k + 1 < FD_COMB_POS_RUN ? FD_WDIG( k + 1 ) : 0;
       FE_FENCE();
-      if( k + 1 < FD_DIAG_COMB_POS ) ctab_fetch_lds( buf, ctab, k + 1, dn );
+      if( k + 1 < FD_COMB_POS_RUN ) ctab_fetch_lds( buf, ctab, k + 1, dn );
       ctab_finish( bp, w, d );
       d = dn;
     }
     FE_FENCE();
-    ge_madd( acc, acc, bp, k + 1 < FD_DIAG_COMB_POS );
+    ge_madd( acc, acc, bp, k + 1 < FD_COMB_POS_RUN );
     FE_FENCE();
   }
 #undef FD_WDIG
@@ -906,6 +906,7 @@ fd_ed25519_verify_kernel( verify_args args ) {
   int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane( tid >> 6 );
 #ifdef FD_PHASE_STAMPS
   uint64_t _st[ FD_NSTAMP ] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+  uint64_t _rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   STAMP( 0 );
   uint64_t gid = (uint64_t)blockIdx.x * (64u * FD_SL_WAVES) + (uint64_t)tid;
@@ -1024,6 +1025,13 @@ fd_ed25519_verify_kernel( verify_args args ) {
     /* 0-1 prologue, 1-2 SHA (live lanes), 2-3 lattice+digits, 3-4 decodes+tables, 4-5 chain+comb, 5-6 compare */
     for( int i=0; i<6; i++ ) atomicAdd( &args.stamps[i], (unsigned long long)(_st[i+1] - _st[i]) );
     atomicAdd( &args.stamps[7], 1ull );
+    /* the wave's clock (MI355X_MICROARCH.md DVFS item 6): s_memtime cycles and
+       s_memrealtime ticks (100 MHz) from start to end, per wave of the launch */
+    uint64_t gw = (uint64_t)blockIdx.x * FD_SL_WAVES + (uint64_t)wv;
+    if( FD_TL_BASE + 2u*gw + 1u < FD_STAMP_WORDS_DEV ) {
+      args.stamps[ FD_TL_BASE + 2u*gw ] = _st[6] - _st[0];
+      args.stamps[ FD_TL_BASE + 2u*gw + 1u ] = __builtin_amdgcn_s_memrealtime() - _rt0;
+    }
   }
 #endif
 }
@@ -1178,11 +1186,6 @@ __device__ __forceinline__ uint32_t len_bucket( fd_ed25519_desc_t const & d ) {
    in the workgroup, so they arrive).  An expired wait stores errv (the
    batch's pipe counter + 1) into *err, the batch's word of the host-mapped
    error ring. */
-#ifdef FD_DIAG_LSORT_TIMEOUT
-#define FD_LSORT_SPIN 0u            /* diagnostic build: every wait that is not already met expires */
-#else
-#define FD_LSORT_SPIN (1u << 20)
-#endif
 __device__ __forceinline__ uint32_t pipe_len_order( uint32_t key, int w, int lane, uint32_t * wh, uint32_t * perm,
                                                     uint32_t * flag, uint32_t * err, uint32_t errv ) {
   uint64_t below = (1ull << lane) - 1ull;
@@ -1340,6 +1343,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_A + j)*cap ] = pub[j];
       h[ (uint64_t)FD_PH_IDX*cap ] = (uint32_t)di;
+      if( a.first_a ) h[ (uint64_t)FD_PH_FRAG*cap ] = (uint32_t)d.txn_idx | ((uint32_t)(di - a.first_a[ d.txn_idx ]) << 16);
     }
     if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)P;     /* the wave's top-digit position */
     FE_FENCE();
@@ -1359,15 +1363,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   uint4 *    buf = s_buf[ role ][ wv ];
   uint32_t * y   = s_y[ role ][ wv ];
   bool phb = role == 1;
-#if defined(FD_DIAG_NT_INV)   /* diagnostic: invalidate this CU's vector L1 (1), the XCC's L2 (2) or both (3) first */
-#if FD_DIAG_NT_INV == 1
-  asm volatile( "buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory" );
-#elif FD_DIAG_NT_INV == 2
-  asm volatile( "buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" );
-#else
-  asm volatile( "buffer_inv sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" );
-#endif
-#endif
+  FD_DIAG_PHASE_BC_ENTRY();
   uint64_t nx = phb ? a.n_b : a.n_c;
   if( (gid & ~(uint64_t)63) >= nx ) return;
   uint64_t set = phb ? a.set_b : a.set_c;
@@ -1415,9 +1411,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       FE_FENCE();
     }
     stA = (int)((m_aok >> lane) & 1u) | (int)(((m_asm >> lane) & 1u) << 1);
-#if defined(FD_DIAG_SC_INV_AFTER)   /* diagnostic: this XCC's L2 invalidated once the tables are stored */
-    asm volatile( "s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory" );
-#endif
+    FD_DIAG_AFTER_TABLES();
     code = verify_precode( args, desc_ok, bad_s, stA, stR );
     if( valid ) a.code_b[ gid ] = (int8_t)code;
   } else {
@@ -1467,7 +1461,34 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
       code = eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
     }
   }
-  if( !phb && valid ) a.out_c[ hand[ (uint64_t)FD_PH_IDX*cap + gid ] ] = (int8_t)code;
+  if( !phb && valid ) {
+    uint32_t di = hand[ (uint64_t)FD_PH_IDX*cap + gid ];
+    a.out_c[ di ] = (int8_t)code;
+    if( a.fold_c ) {
+      /* frag batch: the code's class into its field of the frag's fold word
+         and the count down, one relaxed atomic (no fence: the word is its own
+         record); the add that ends the count writes the frag's record */
+      uint32_t fw = hand[ (uint64_t)FD_PH_FRAG*cap + gid ];
+      uint32_t fi = fw & 0xffffu, k = fw >> 16;
+      uint64_t cls = code == FD_ED25519_SUCCESS ? 0u : code == FD_ED25519_ERR_MSG ? 1u : code == FD_ED25519_ERR_SIG ? 2u :
+                     code == FD_ED25519_ERR_PUBKEY ? 3u : 4u;
+      uint64_t delta = (cls << (FD_FOLD_SH + 3u*k)) - 1u;
+      uint64_t old = __hip_atomic_fetch_add( a.fold_c + fi, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+      if( (old & 0xffu) == 1u ) {
+        uint64_t w = (old + delta) >> FD_FOLD_SH;
+        int st = FD_ED25519_SUCCESS, any_msg = 0;
+#pragma unroll 1
+        for( int j=0; j<16; j++, w >>= 3 ) {       /* first phase-1 error by index, else ERR_MSG, else SUCCESS */
+          uint32_t c = (uint32_t)w & 7u;
+          if( c == 1u ) any_msg = 1;
+          else if( c ) { st = c == 2u ? FD_ED25519_ERR_SIG : c == 3u ? FD_ED25519_ERR_PUBKEY : FD_ED25519_GPU_CODE_BAD_DESC; break; }
+        }
+        if( st == FD_ED25519_SUCCESS && any_msg ) st = FD_ED25519_ERR_MSG;
+        uint64_t tag = a.ftag_c[ fi ];
+        ((uint4 *)a.frec_c)[ fi ] = make_uint4( (uint32_t)tag, (uint32_t)(tag >> 32), (uint32_t)(int32_t)st, 0u );
+      }
+    }
+  }
 #ifdef FD_PHASE_STAMPS
   if( args.stamps && lane == 0 ) { atomicAdd( &args.stamps[phb ? 1 : 0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0) ); atomicAdd( &args.stamps[phb ? 6 : 7], 1ull ); }
 #endif
@@ -1880,110 +1901,136 @@ __device__ __forceinline__ uint32_t frag_block_scan( uint32_t x, uint32_t * wsum
   return pre + v - x;
 }
 
-/* The per-frag parse plus the descriptor-index scan in one launch (the
-   separate single-workgroup scan kernel took 44 us of a 35K-frag batch,
-   profiles/r04/stage): each workgroup writes its frags' workgroup-relative
-   first descriptor index into cnt and its descriptor total into bpre; the
-   last workgroup to finish (a device-scope counter, reset by that workgroup
-   for the next batch) turns bpre into the workgroups' first indices and
-   writes the batch's total.  Frag i's first descriptor is then
-   cnt[i] + bpre[i / FD_FRAG_BLOCK].  No workgroup waits for another. */
+/* Decoupled look-back (single-pass scan across tiles of FD_FRAG_BLOCK
+   frags): tile t publishes its aggregate, then sums its predecessors' words
+   64 at a time (one per lane) until one of them carries an inclusive
+   prefix, and publishes its own.  Word: epoch (32) | status (2: 1
+   aggregate, 2 inclusive prefix) | value (30); a word of an older epoch is
+   "not yet".  Called by one whole wave; returns the exclusive prefix
+   (uniform).  The wait is bounded (*late on expiry; the batch then fails). */
+#define FD_LB_AGG    1ull
+#define FD_LB_PREFIX 2ull
+#define FD_LB_SPIN   (1u << 22)
+__device__ __forceinline__ uint32_t frag_lookback( uint64_t * flag, uint64_t t, uint32_t agg, uint32_t epoch, int * late ) {
+  uint32_t lane = threadIdx.x & 63u;
+  uint64_t ep = (uint64_t)epoch << 32;
+  if( t == 0u ) {
+    if( lane == 0u ) __hip_atomic_store( flag, ep | (FD_LB_PREFIX << 30) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+    return 0u;
+  }
+  if( lane == 0u ) __hip_atomic_store( flag + t, ep | (FD_LB_AGG << 30) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  uint32_t excl = 0u, spin = 0u;
+  int64_t top = (int64_t)t - 1;
+  for(;;) {
+    int64_t k = top - (int64_t)lane;             /* lane l reads predecessor top - l; none left: a prefix of 0 */
+    uint64_t w = k >= 0 ? __hip_atomic_load( flag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) : (ep | (FD_LB_PREFIX << 30));
+    uint64_t stt = (w >> 30) & 3ull;
+    bool ready = (w & 0xffffffff00000000ull) == ep && stt != 0ull;
+    uint64_t pre = __ballot( ready && stt == FD_LB_PREFIX );
+    uint64_t need = pre ? ((pre & (~pre + 1ull)) << 1) - 1ull : ~0ull;   /* lanes up to the nearest prefix */
+    if( __ballot( !ready ) & need ) {
+      if( ++spin > FD_LB_SPIN ) { *late = 1; break; }
+      __builtin_amdgcn_s_sleep( 1 );
+      continue;
+    }
+    uint32_t v = ((need >> lane) & 1ull) ? (uint32_t)(w & 0x3fffffffull) : 0u;
+#pragma unroll
+    for( int o=32; o>=1; o>>=1 ) v += __shfl_xor( v, o );
+    excl += v;
+    if( pre ) break;
+    top -= 64;
+  }
+  if( lane == 0u )
+    __hip_atomic_store( flag + t, ep | (FD_LB_PREFIX << 30) | ((excl + agg) & 0x3fffffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  return excl;
+}
+
+/* The per-frag parse, the descriptor-index scan and the descriptors in one
+   launch (round 4 ran parse + scan, then an emit launch; the fold of the
+   codes now runs in the pipelined kernel's phase C).  Workgroup g takes
+   tiles g, g + G, g + 2G, ... (G = the grid, at most one workgroup per CU,
+   all co-resident): each tile scans its frags' signature counts, takes its
+   base from the look-back over the tiles before it -- tile t's
+   predecessors are earlier tiles of co-resident workgroups, each of which
+   runs its tiles in order, so every wait ends whatever order the workgroups
+   were dispatched in -- and every lane writes its frag's descriptors at
+   base + its exclusive count; the last tile writes the batch's total.  Per
+   frag: status, tag, first descriptor index, and the fold words (min key
+   ~0, the descriptor count) the phase-C fold counts down. */
 extern "C" __global__ void __launch_bounds__( FD_FRAG_BLOCK )
 fd_frag_parse_kernel( fparse_args a ) {
   __shared__ uint32_t wsum[ FD_FRAG_BLOCK / 64u ];
-  __shared__ uint32_t is_last;
-  uint64_t i = (uint64_t)blockIdx.x * FD_FRAG_BLOCK + threadIdx.x;
-  fd_ed25519_gpu_frag_t f; f.off = 0xffffffffu; f.sz = 0u;
-  if( i < a.n ) f = a.frag[ i ];
-  int st = FD_TXN_VERIFY_BAD_FRAG;
-  uint64_t tag = 0u;
-  uint32_t cnt = 0u, so = 0u, po = 0u, mo = 0u, ms = 0u;
-  uint64_t off = f.off, sz = f.sz;
-  do {
-    if( off > a.arena_sz || sz > a.arena_sz - off || sz < 2u ) break;          /* fd_verify.c:94-96 */
-    if( off < a.span_lo || off + sz > a.span_lo + a.span_sz ) break;
-    uint64_t ro = off - a.span_lo;                                              /* span-relative */
-    uint64_t psz = span_ld16( a.span + ro + sz - 2u );                          /* :98 */
-    if( psz > 2086u ) break;                                                    /* :101-103 */
-    uint64_t t = ro + psz + ((a.host_parity + off + psz) & 1u);                  /* :108 align_up( addr, 2 ) */
-    if( t + 14u > a.span_sz ) break;
-    uint8_t const * txn = a.span + t;
-    if( span_ld16( txn + 12 ) >= psz ) break;                                   /* :112-115 */
-    uint64_t c = txn[1];
-    uint64_t s_ = ro + span_ld16( txn + 2 ), p_ = ro + span_ld16( txn + 10 ), m_ = span_ld16( txn + 4 );
-    if( s_ + 8u > a.span_sz ) break;
-    uint8_t const * sg = a.span + s_;
+  __shared__ uint32_t s_base;
+  uint64_t ntile = (a.n + FD_FRAG_BLOCK - 1u) / FD_FRAG_BLOCK;
+  for( uint64_t tl=blockIdx.x; tl<ntile; tl+=gridDim.x ) {
+    uint64_t i = tl * FD_FRAG_BLOCK + threadIdx.x;
+    fd_ed25519_gpu_frag_t f; f.off = 0xffffffffu; f.sz = 0u;
+    if( i < a.n ) f = a.frag[ i ];
+    int st = FD_TXN_VERIFY_BAD_FRAG;
+    uint64_t tag = 0u;
+    uint32_t cnt = 0u, so = 0u, po = 0u, mo = 0u, ms = 0u;
+    uint64_t off = f.off, sz = f.sz;
+    do {
+      if( off > a.arena_sz || sz > a.arena_sz - off || sz < 2u ) break;          /* fd_verify.c:94-96 */
+      if( off < a.span_lo || off + sz > a.span_lo + a.span_sz ) break;
+      uint64_t ro = off - a.span_lo, re = ro + sz;                                /* the frag, span-relative */
+      uint64_t psz = span_ld16( a.span + re - 2u );                               /* :98 */
+      if( psz > 2086u ) break;                                                    /* :101-103 */
+      uint64_t t = ro + psz + ((a.host_parity + off + psz) & 1u);                  /* :108 align_up( addr, 2 ) */
+      if( t + 14u > re ) break;                    /* every field read lies inside the frag (fd_txn_parse output does) */
+      uint8_t const * txn = a.span + t;
+      if( span_ld16( txn + 12 ) >= psz ) break;                                   /* :112-115 */
+      uint64_t c = txn[1];
+      uint64_t s_ = ro + span_ld16( txn + 2 ), p_ = ro + span_ld16( txn + 10 ), m_ = span_ld16( txn + 4 );
+      if( s_ + 8u > re ) break;
+      uint8_t const * sg = a.span + s_;
 #pragma unroll
-    for( int b=7; b>=0; b-- ) tag = (tag << 8) | sg[b];
-    if( m_ > psz ) break;
-    if( !c || c > 16u ) { st = FD_TXN_VERIFY_FAILED; break; }                  /* batch_sz 0 or > 16 -> ERR_SIG */
-    if( c * FD_FRAG_SIG_BYTES > sz ) break;                                     /* more signatures than the frag holds */
-    if( s_ + 64u*c > a.span_sz || p_ + 32u*c > a.span_sz ) break;
-    st = 0; cnt = (uint32_t)c; so = (uint32_t)s_; po = (uint32_t)p_; mo = (uint32_t)(ro + m_); ms = (uint32_t)(psz - m_);
-  } while( 0 );
-  uint32_t btot;
-  uint32_t excl = frag_block_scan( cnt, wsum, &btot );
-  if( i < a.n ) {
-    a.status[ i ] = (int8_t)st; a.tag[ i ] = tag; a.cnt[ i ] = excl;
-    uint4 fl; fl.x = so; fl.y = po; fl.z = mo; fl.w = ms;
-    ((uint4 *)a.fld)[ i ] = fl;
-  }
-  if( threadIdx.x == 0u ) {
-    a.bpre[ blockIdx.x ] = btot;
-    /* release: this workgroup's total is visible before the count says so;
-       acquire: the last one sees every workgroup's total */
-    uint32_t old = __hip_atomic_fetch_add( a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT );
-    is_last = old == gridDim.x - 1u;
-  }
-  __syncthreads();
-  if( !is_last ) return;
-  __threadfence();
-  uint32_t run = 0u;
-  for( uint32_t b0=0; b0<gridDim.x; b0+=FD_FRAG_BLOCK ) {
-    uint32_t j = b0 + threadIdx.x;
-    uint32_t v = j < gridDim.x ? a.bpre[ j ] : 0u;
-    uint32_t ctot;
-    uint32_t e = frag_block_scan( v, wsum, &ctot );
-    if( j < gridDim.x ) a.bpre[ j ] = run + e;
-    run += ctot;
-  }
-  if( threadIdx.x == 0u ) { *a.total = run; *a.done = 0u; }
-}
-
-/* Frag i's first descriptor index (i == n: the batch's total). */
-__device__ __forceinline__ uint64_t frag_first( fparse_args const & a, uint64_t i ) {
-  return i < a.n ? (uint64_t)a.cnt[ i ] + (uint64_t)a.bpre[ i / FD_FRAG_BLOCK ] : (uint64_t)*a.total;
-}
-
-/* Descriptors of every frag at its scanned position (txn_idx = frag index). */
-extern "C" __global__ void __launch_bounds__( FD_FRAG_BLOCK )
-fd_frag_emit_kernel( fparse_args a ) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if( i >= a.n || a.status[ i ] ) return;
-  uint32_t const * fl = a.fld + 4u*i;
-  uint64_t at = frag_first( a, i );
-  uint32_t c = (uint32_t)(frag_first( a, i + 1u ) - at);
-  for( uint32_t j=0; j<c && at + j < a.desc_cap; j++ ) {
-    fd_ed25519_desc_t d;
-    d.sig_off = fl[0] + 64u*j; d.pub_off = fl[1] + 32u*j; d.msg_off = fl[2];
-    d.msg_sz = (uint16_t)fl[3]; d.txn_idx = (uint16_t)i;
-    a.desc[ at + j ] = d;
+      for( int b=7; b>=0; b-- ) tag = (tag << 8) | sg[b];
+      if( m_ > psz || psz > sz ) break;
+      if( !c || c > 16u ) { st = FD_TXN_VERIFY_FAILED; break; }                  /* batch_sz 0 or > 16 -> ERR_SIG */
+      if( c * FD_FRAG_SIG_BYTES > sz ) break;                                     /* more signatures than the frag holds */
+      if( s_ + 64u*c > re || p_ + 32u*c > re ) break;
+      st = 0; cnt = (uint32_t)c; so = (uint32_t)s_; po = (uint32_t)p_; mo = (uint32_t)(ro + m_); ms = (uint32_t)(psz - m_);
+    } while( 0 );
+    uint32_t btot;
+    uint32_t excl = frag_block_scan( cnt, wsum, &btot );                        /* (its first barrier frees s_base) */
+    if( threadIdx.x < 64u ) {                                                   /* wave 0: the look-back */
+      int late = 0;
+      uint32_t base = frag_lookback( a.flag, tl, btot, a.epoch, &late );
+      if( threadIdx.x == 0u ) {
+        s_base = base;
+        if( late && a.err ) __hip_atomic_store( a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+        if( tl == ntile - 1u ) *a.total = base + btot;
+      }
+    }
+    __syncthreads();
+    uint32_t first = s_base + excl;
+    if( i < a.n ) {
+      a.status[ i ] = (int8_t)st; a.tag[ i ] = tag; a.first[ i ] = first;
+      a.fold[ i ] = cnt;
+      if( st ) ((uint4 *)a.hrec)[ i ] = make_uint4( (uint32_t)tag, (uint32_t)(tag >> 32), (uint32_t)(int32_t)st, 0u );   /* no descriptors: final */
+      for( uint32_t j=0; j<cnt && (uint64_t)first + j < a.desc_cap; j++ ) {
+        fd_ed25519_desc_t d;
+        d.sig_off = so + 64u*j; d.pub_off = po + 32u*j; d.msg_off = mo;
+        d.msg_sz = (uint16_t)ms; d.txn_idx = (uint16_t)i;
+        a.desc[ first + j ] = d;
+      }
+    }
   }
 }
 
 /* Each frag's verify code from its descriptors' codes, with
    fd_ed25519_verify_batch_single_msg's precedence (first phase-1 error,
-   else ERR_MSG, else SUCCESS), into status[i] for frags that had
-   descriptors; every frag's status and tag then go straight into the
-   host's page-locked staging (hstatus, htag: no copy launches after the
-   fold -- two of them plus their queue gaps were ~45 us a batch). */
+   else ERR_MSG, else SUCCESS), for batches verified by the one-shot kernels
+   (the pipelined kernel folds in its phase C); every frag's status and tag
+   go straight into the host's page-locked staging. */
 extern "C" __global__ void __launch_bounds__( FD_FRAG_BLOCK )
 fd_frag_fold_kernel( fparse_args a ) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= a.n ) return;
   int st = a.status[ i ];
   if( !st ) {
-    uint64_t at = frag_first( a, i ), end = frag_first( a, i + 1u );
+    uint64_t at = a.first[ i ], end = at + (a.fold[ i ] & 0xffu);
     int first = 0, any_msg = 0;
     for( uint64_t k=at; k<end; k++ ) {
       int c = a.code[ k ];
@@ -1992,8 +2039,8 @@ fd_frag_fold_kernel( fparse_args a ) {
     }
     st = first ? first : (any_msg ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS);
   }
-  a.hstatus[ i ] = (int8_t)st;
-  a.htag[ i ] = a.tag[ i ];
+  uint64_t tag = a.tag[ i ];
+  ((uint4 *)a.hrec)[ i ] = make_uint4( (uint32_t)tag, (uint32_t)(tag >> 32), (uint32_t)(int32_t)st, 0u );
 }
 
 /* Self-test kernel (tests only, fd_ed25519_gpu_test_lattice): the device

@@ -21,6 +21,8 @@
 #include <string.h>
 #include <vector>
 
+extern "C" int fd_ed25519_gpu_host_register_auto( fd_ed25519_gpu_t * ctx, void * p, uint64_t sz );   /* host.cpp */
+
 static inline uint64_t now_ns( void ) {
   struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
@@ -32,8 +34,11 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
                          uint64_t * stats /* [7]: batches, frags, max batch, idle polls, ns in submit, ns in
                                              completing polls, ns first frag -> last result */ ) {
   if( !off || !ctx || !tc || !max_batch ) return FD_ED25519_GPU_ERR_ARG;
+  /* the shared frag area lives as long as the link: page-locked once here,
+     so the stage's span copies are DMA (released below if registered here) */
+  int reg = fd_ed25519_gpu_host_register_auto( ctx, fd_verify_offload_dcache( off ), fd_verify_offload_dcache_sz( off ) );
   fd_ed25519_gpu_stage_t * st = fd_ed25519_gpu_stage_new( ctx, tc, max_batch, threads );
-  if( !st ) return FD_ED25519_GPU_ERR_OOM;
+  if( !st ) { if( reg == 0 ) fd_ed25519_gpu_host_unregister( ctx, fd_verify_offload_dcache( off ) ); return FD_ED25519_GPU_ERR_OOM; }
   enum { DEPTH = FD_ED25519_GPU_STAGE_DEPTH };   /* the stage's batches outstanding */
   uint64_t q_seq[ DEPTH ], q_cnt[ DEPTH ];   /* outstanding batches, oldest first */
   int q = 0;
@@ -92,6 +97,7 @@ fd_verify_offload_serve( fd_verify_offload_t * off, fd_ed25519_gpu_t * ctx, fd_e
     }
   }
   fd_ed25519_gpu_stage_delete( st );
+  if( reg == 0 ) fd_ed25519_gpu_host_unregister( ctx, dc );
   if( stats ) {
     stats[0] = s_batches; stats[1] = s_frags; stats[2] = s_max; stats[3] = s_idle;
     stats[4] = s_sub_ns; stats[5] = s_poll_ns; stats[6] = t_last - t_first;

@@ -295,7 +295,11 @@ frag_parse( uint8_t const * arena, uint64_t arena_sz, fd_ed25519_gpu_frag_t f, u
   if( payload_sz > FD_TPU_DCACHE_MTU_ ) return FD_TXN_VERIFY_BAD_FRAG;               /* :101-103 */
   uint64_t txn_addr = ((uintptr_t)pay + payload_sz + 1u) & ~(uintptr_t)1;          /* :108 */
   uint64_t txn_off  = txn_addr - (uintptr_t)arena;
-  if( txn_off + TXN_HDR_SZ > arena_sz ) return FD_TXN_VERIFY_BAD_FRAG;
+  /* every field read below lies inside the frag [off, end) (fd_txn_parse
+     output always does; a field outside it is BAD_FRAG here and in the device
+     parse, which sees only the page runs the batch's frags occupy) */
+  uint64_t end = off + sz;
+  if( txn_off + TXN_HDR_SZ > end ) return FD_TXN_VERIFY_BAD_FRAG;
   uint8_t const * txn = arena + txn_off;
   if( ld16( txn + TXN_RBH_OFF ) >= payload_sz ) return FD_TXN_VERIFY_BAD_FRAG;      /* :112-115 */
 
@@ -304,16 +308,17 @@ frag_parse( uint8_t const * arena, uint64_t arena_sz, fd_ed25519_gpu_frag_t f, u
   uint64_t soff = off + ld16( txn + TXN_SIG_OFF  );
   uint64_t aoff = off + ld16( txn + TXN_ACCT_OFF );
   uint64_t moff = ld16( txn + TXN_MSG_OFF );
-  if( soff + 8u > arena_sz ) return FD_TXN_VERIFY_BAD_FRAG;
+  if( soff + 8u > end ) return FD_TXN_VERIFY_BAD_FRAG;
   *tag = ld64( arena + soff );
   if( moff > payload_sz ) return FD_TXN_VERIFY_BAD_FRAG;      /* msg_sz would wrap (reference reads ~2^64 B) */
+  if( payload_sz > sz ) return FD_TXN_VERIFY_BAD_FRAG;        /* the message runs past the frag */
   if( !cnt || cnt > 16u ) return FD_TXN_VERIFY_FAILED;        /* batch_sz==0 || >16 -> ERR_SIG, fd_ed25519_user.c */
   /* more signatures than the frag can hold (each needs its 64 bytes and its
      signer's 32-byte address in the payload): impossible for fd_txn_parse
      output; BAD_FRAG here as in the device parse, whose verify grid is
      sized by this bound (FD_FRAG_SIG_BYTES) */
   if( cnt * 96u > sz ) return FD_TXN_VERIFY_BAD_FRAG;
-  if( soff + 64u * cnt > arena_sz || aoff + 32u * cnt > arena_sz ) return FD_TXN_VERIFY_BAD_FRAG;
+  if( soff + 64u * cnt > end || aoff + 32u * cnt > end ) return FD_TXN_VERIFY_BAD_FRAG;
   if( arena_sz > 0xffffffffull ) return FD_TXN_VERIFY_BAD_FRAG;  /* descriptor offsets are u32 */
   *sig_off = (uint32_t)soff; *pub_off = (uint32_t)aoff;
   *msg_off = (uint32_t)(off + moff); *msg_sz = (uint32_t)(payload_sz - moff);
@@ -414,7 +419,7 @@ struct fd_ed25519_gpu_stage {
   uint64_t                  max_frags;
   int                       threads;
   int                       devparse;      /* parse frags on the GPU when the context has room */
-  int                       autoreg;       /* page-lock callers' frag areas (default on) */
+  int                       autoreg;       /* page-lock callers' frag areas (opt-in: FD_ED25519_GPU_STAGE_AUTOREG=1) */
   int                       head;          /* oldest pending slot */
   int                       pending;       /* 0..FD_VS_DEPTH */
   vs_batch                  b[ FD_VS_DEPTH ];
@@ -703,10 +708,15 @@ vs_replayer( fd_ed25519_gpu_stage_t * st ) {
   }
 }
 
-/* Page-locks the caller's frag area once (hipHostRegister), so each span
-   copy to HBM is a DMA instead of a staged copy on the calling thread.  A
-   range the caller registered already (HIP says so) is fine as it is.  Best
-   effort: a failure leaves the area pageable. */
+/* Opt-in (FD_ED25519_GPU_STAGE_AUTOREG=1): page-locks the caller's frag area
+   once (hipHostRegister), so each span copy to HBM is a DMA instead of a
+   staged copy on the calling thread, and keeps it registered until
+   stage_delete -- so the caller must keep the area alive, and not register
+   it itself, for the stage's whole lifetime.  Off by default: a caller
+   registers its long-lived frag area (the dcache) with
+   fd_ed25519_gpu_host_register, as the offload server does.  A range the
+   caller registered already (HIP says so) is left alone.  Best effort: a
+   failure leaves the area pageable. */
 static void
 vs_autoreg( fd_ed25519_gpu_stage_t * st, uint8_t const * arena, uint64_t arena_sz ) {
   if( !st->autoreg || !arena || !arena_sz ) return;
@@ -730,8 +740,8 @@ fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, 
   st->ctx = ctx; st->tc = tc; st->max_frags = max_frags;
   st->threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
   st->devparse = 1;
-  char const * e = getenv( "FD_ED25519_GPU_STAGE_AUTOREG" );        /* "0": leave frag areas pageable (A/B) */
-  st->autoreg = !(e && e[0] == '0');
+  char const * e = getenv( "FD_ED25519_GPU_STAGE_AUTOREG" );        /* "1": page-lock callers' frag areas */
+  st->autoreg = e && e[0] == '1';
   memset( &st->stats, 0, sizeof(st->stats) );
   /* size the device-parse buffers now, not while a batch is in flight
      (best effort: a context too small for max_frags parses on the host) */
@@ -806,12 +816,15 @@ fd_ed25519_gpu_stage_submit( fd_ed25519_gpu_stage_t * st, uint8_t const * arena,
   if( b->devp ) {
     b->n = frag_cnt; b->harena = arena; b->harena_sz = arena_sz; b->hfrag = frag; b->ndesc = 0;
     b->tag.resize( frag_cnt );
-  } else {
+  }
+  uint64_t parse_ns = 0u;
+  if( !b->devp ) {
     uint64_t tp = vs_now();
     vs_parse( b, arena, arena_sz, frag, frag_cnt, st->threads );
-    st->stats.parse_ns += vs_now() - tp;
+    parse_ns = vs_now() - tp;
   }
   std::lock_guard<std::mutex> lk( st->mu );
+  st->stats.parse_ns += parse_ns;            /* the stats are read and reset under the lock */
   if( b->devp ) vs_autoreg( st, arena, arena_sz );
   b->state = 1;
   st->pending++;

@@ -146,10 +146,12 @@ class AsyncStage:
         r = self.lib.fd_ed25519_gpu_stage_poll(self.st, 1 if block else 0)
         if r == 1:
             return False
-        if r:
-            raise GpuError("fd_ed25519_gpu_stage_poll: %s (%d)" % (strerror(r), r))
+        # any other return retired the oldest batch (a failed batch too: the
+        # stage goes on with the next one), so its buffers go with it
         if self._keep:
             self._keep.pop(0)
+        if r:
+            raise GpuError("fd_ed25519_gpu_stage_poll: %s (%d)" % (strerror(r), r))
         return True
 
     def pending(self):

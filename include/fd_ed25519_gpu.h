@@ -92,7 +92,10 @@ typedef struct fd_ed25519_gpu fd_ed25519_gpu_t;
    split internally).  Every slot reads a 5.9 GB fixed-base comb table, ONE
    per device per process, shared by all slots and contexts on it (built by
    the first one, ~0.08 s; freed with the last) beside the slot's
-   max_batch-sized buffers.  Returns NULL on failure (no device / OOM). */
+   max_batch-sized buffers.  max_batch <= FD_ED25519_GPU_MAX_BATCH (2^23;
+   0 = 2^18).  Returns NULL on failure (no device / OOM / max_batch too
+   large). */
+#define FD_ED25519_GPU_MAX_BATCH (1ull << 23)
 fd_ed25519_gpu_t * fd_ed25519_gpu_new( uint64_t device_mask, uint64_t max_batch );
 /* Same over an explicit list of shard slots: slot j runs on HIP device
    dev_ids[j] with its own stream, tables and scratch; a device may appear
@@ -367,10 +370,12 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
    stage and go to the GPU as earlier ones complete.  Batches
    complete strictly in submission order, which keeps the tile's frag order
    for the tcache.  The frag bytes and the result / sig arrays of a batch
-   must stay valid until its poll returns.  By default the stage page-locks
-   each frag area it is given (once; released by stage_delete;
-   FD_ED25519_GPU_STAGE_AUTOREG=0 leaves it pageable), so the span copies
-   to HBM are DMA from the caller's memory.  The stage owns ctx while it
+   must stay valid until its poll returns.  Register a long-lived frag area
+   (the dcache) once with fd_ed25519_gpu_host_register so the span copies to
+   HBM are DMA from it (pageable areas work, through staged copies);
+   FD_ED25519_GPU_STAGE_AUTOREG=1 makes the stage page-lock each frag area it
+   is given itself, keeping it registered until stage_delete (the area must
+   then outlive the stage).  The stage owns ctx while it
    lives: no other call on ctx while batches are pending (the poller uses
    it from its own thread). */
 typedef struct fd_ed25519_gpu_stage fd_ed25519_gpu_stage_t;
@@ -587,6 +592,16 @@ int fd_ed25519_gpu_test_ctab_stats( int dev, uint64_t * refs, uint64_t * builds 
 int fd_ed25519_gpu_test_copy_plan( int kind, void const * items, uint64_t n, uint8_t const * arena, uint64_t arena_sz,
                                    int nslot, uint64_t * bytes, uint64_t * runs,
                                    uint8_t * image, uint64_t image_cap, void * rebased );
+
+/* Bench hook (host only, no device; not part of the reference interface):
+   the host work of a multi-slot submit of n descriptors (kind 0) or frags
+   (kind 1) over nslot slots -- each slot's copy plan and rebased records, on
+   per-slot threads as fd_ed25519_gpu_submit / the frag path run them --
+   iters times after one untimed pass; copy = 1 also memcpys the page runs
+   (the CPU standing in for the DMA engines).  *ns = wall time of the timed
+   passes, *bytes = the bytes one pass's runs would send to HBM. */
+int fd_ed25519_gpu_test_submit_host( int kind, void const * items, uint64_t n, uint8_t const * arena, uint64_t arena_sz,
+                                     int nslot, int iters, int copy, uint64_t * ns, uint64_t * bytes );
 
 /* Test hook (not part of the reference interface): the verify stage's
    in-order tcache steps (fd_verify.h:63-86) over n frags -- res[i] the

@@ -263,6 +263,47 @@ def _corrupt_frags(arena, frags, kind, i):
 BAD_KINDS = ["short", "mtu", "rbh", "nosig", "manysig", "outside", "overclaim", None]
 
 
+def _fields_outside_stream():
+    """Frags whose fd_txn_t points a field past the frag's own bytes (ADVICE
+    r04: the device parse sees only the page runs the batch's frags occupy,
+    gaps over 16 pages dropped): frag 1's signatures ~58 KB past it, inside
+    a 20-page hole before frag 3 (so the device span's bytes there belong to
+    another run); frag 2's signer keys past its end; frag 4's payload_sz
+    past the frag.  Valid frags 0, 3 and 5 around them.  Expected: BAD_FRAG
+    for 1, 2 and 4 in both parses."""
+    fx = fixture_txns()
+    txns = [fx["valid_txn_1sig"], fx["valid_txn_2sigs"], fx["valid_txn_1sig"]]
+    a0, f0 = _mk_frags(txns)
+    a1, f1 = _mk_frags([fx["valid_txn_2sigs"], fx["valid_txn_1sig"], fx["valid_txn_1sig"]])
+    hole = 20 * 4096
+    arena = np.zeros(len(a0) + hole + len(a1), np.uint8)
+    arena[:len(a0)] = a0
+    arena[len(a0) + hole:] = a1
+    frags = np.zeros(6, f0.dtype)
+    frags[:3] = f0
+    frags["off"][3:] = f1["off"] + len(a0) + hole
+    frags["sz"][3:] = f1["sz"]
+    def txn_at(i):
+        off, sz = int(frags["off"][i]), int(frags["sz"][i])
+        psz = struct.unpack_from("<H", arena, off + sz - 2)[0]
+        return off, sz, off + psz + (psz & 1)
+    off, sz, t = txn_at(1)
+    struct.pack_into("<H", arena, t + 2, 58000)                  # signature_off ~14 pages past frag 1
+    arena[off + 58000:off + 58000 + 8] = 0x5a                    # (host bytes there: a nonzero tag)
+    off, sz, t = txn_at(2)
+    struct.pack_into("<H", arena, t + 10, sz - 16)               # acct_addr_off: the keys run past the frag
+    off, sz, t = txn_at(4)
+    struct.pack_into("<H", arena, off + sz - 2, sz + 8)          # payload_sz past the frag
+    return arena, frags
+
+
+def test_frags_fields_outside_frag_bad():
+    """Host parse: every field it reads must lie inside the frag."""
+    arena, frags = _fields_outside_stream()
+    desc, st, tag = fa.frags_to_descs(arena, len(arena), frags)
+    assert list(st) == [0, BAD, BAD, 0, BAD, 0], list(st)
+
+
 def test_frags_to_descs_bad_frags():
     fx = fixture_txns()
     arena, frags = _mk_frags([fx["valid_txn_1sig"]] * len(BAD_KINDS))
@@ -520,6 +561,51 @@ def test_stage_device_parse_bad_frags(gpu):
         out[devparse] = (res.copy(), sig.copy())
     assert list(out[True][0]) == [BAD, BAD, BAD, F, F, BAD, BAD, S, S]
     assert np.array_equal(out[True][0], out[False][0]) and np.array_equal(out[True][1], out[False][1])
+
+
+@pytest.mark.gpu
+def test_stage_device_parse_fields_outside_frag(gpu):
+    """Device parse = host parse on frags whose fields point past the frag
+    (one of them across a hole the copy plan does not send): BAD_FRAG in
+    both, the valid frags around them verified."""
+    arena, frags = _fields_outside_stream()
+    out = {}
+    for devparse in (True, False):
+        ast = fa.AsyncStage(gpu, fa.TCache(), 64, threads=1, device_parse=devparse)
+        res = np.zeros(len(frags), np.int8); sig = np.zeros(len(frags), np.uint64)
+        ast.submit(arena, len(arena), np.ascontiguousarray(frags), res, sig)
+        while ast.pending():
+            ast.poll(True)
+        ast.close()
+        out[devparse] = (res.copy(), sig.copy())
+    assert list(out[True][0]) == [S, BAD, BAD, S, BAD, D], list(out[True][0])
+    assert np.array_equal(out[True][0], out[False][0]) and np.array_equal(out[True][1], out[False][1])
+
+
+@pytest.mark.gpu
+def test_stage_frag_areas_freed_between_batches(gpu):
+    """The stage does not page-lock callers' frag areas by default (ADVICE
+    r04): a frag area freed after its batch's poll and a new one (possibly at
+    the same addresses) give correct results, and the caller can register
+    the new area itself afterwards (it is not left registered by the stage)."""
+    fx = fixture_txns()
+    ast = fa.AsyncStage(gpu, fa.TCache(), 64, threads=1, device_parse=True)
+    try:
+        for rnd in range(3):
+            names = ["valid_txn_1sig", "valid_txn_2sigs", "invalid_txn_2sigs"]
+            arena, frags = _mk_frags([fx[k] for k in names])
+            arena = arena.copy()
+            res = np.zeros(len(frags), np.int8); sig = np.zeros(len(frags), np.uint64)
+            ast.tcache.reset()
+            ast.submit(arena, len(arena), np.ascontiguousarray(frags), res, sig)
+            while ast.pending():
+                ast.poll(True)
+            assert list(res) == [S, S, F], (rnd, list(res))
+            gpu.host_register(arena)          # fails with AlreadyRegistered if the stage had kept it
+            gpu.host_unregister(arena)
+            del arena, frags
+    finally:
+        ast.close()
 
 
 @pytest.mark.gpu

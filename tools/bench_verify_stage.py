@@ -103,16 +103,15 @@ def main():
 
     def measure(pipe):
         """(frags/s, results, launches, breakdown) of the async stage: with the
-        stage's default page-locking of the frag area, then with the frag
-        area left pageable (FD_ED25519_GPU_STAGE_AUTOREG=0)"""
+        frag area page-locked by the caller (fd_ed25519_gpu_host_register, as a
+        tile registers its dcache once), then left pageable"""
         os.environ["FD_ED25519_GPU_ASYNC_PIPE"] = "1" if pipe else "0"
         out = {}
         for mode in ("registered", "pageable"):
-            if mode == "pageable":
-                os.environ["FD_ED25519_GPU_STAGE_AUTOREG"] = "0"
             big = fa.Ed25519Gpu(device_mask=1, max_batch=16 * ab)
+            if mode == "registered":
+                big.host_register(arena)
             ast = fa.AsyncStage(big, fa.TCache(), ab, threads=8, device_parse=True)
-            os.environ.pop("FD_ED25519_GPU_STAGE_AUTOREG", None)
             res_a = np.zeros(len(frags), np.int8); sig_a = np.zeros(len(frags), np.uint64)
             calls = {"submit_s": 0.0, "poll_s": 0.0}
 
@@ -175,7 +174,10 @@ def main():
                                     "passes": args.steps, "results_differing_from_single_pass": diff}
             else:
                 assert np.array_equal(res_a, res_reg)
-            ast.close(); big.close()
+            ast.close()
+            if mode == "registered":
+                big.host_unregister(arena)
+            big.close()
         os.environ.pop("FD_ED25519_GPU_ASYNC_PIPE", None)
         return out, res_reg, launches
     pipe_m, res_a, launches = measure(True)
@@ -191,8 +193,8 @@ def main():
             "async_device_parse": {"batch": ab, "in_flight": fa.QUEUE_DEPTH, "stage_depth": fa.STAGE_DEPTH, "kernel": "pipelined",
                                    "launches_pipe_oneshot": launches, **pipe_m,
                                    "results": {int(k): int(v) for k, v in zip(*np.unique(res_a, return_counts=True))},
-                                   "note": "registered: the stage page-locks the frag area itself (default); "
-                                           "pageable: FD_ED25519_GPU_STAGE_AUTOREG=0.  stage_ms_per_run: the "
+                                   "note": "registered: the caller page-locked the frag area "
+                                           "(fd_ed25519_gpu_host_register); pageable: not.  stage_ms_per_run: the "
                                            "caller's submit / poll and the completion worker's GPU polls, back-off "
                                            "waits and tcache replays; submit_path_ms_per_run: inside the GPU submits; "
                                            "streaming: --steps passes over the frags as one stream, no pipeline "

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../firedancer_amd"
 mkdir -p ../tools/bin
 for spec in "$@"; do
   name=${spec%%=*}; defs=${spec#*=}
-  make -s VARIANT=var_$name EXTRA_DEFS="$defs" OUT=../tools/bin/libvar_$name.so ../tools/bin/libvar_$name.so 2>&1 | grep -v "hip-link\|asm_peephole" || true
+  make -s VARIANT=var_$name EXTRA_DEFS="-DFD_DIAG_BUILD $defs" OUT=../tools/bin/libvar_$name.so ../tools/bin/libvar_$name.so 2>&1 | grep -v "hip-link\|asm_peephole" || true
   python3 - build/var_$name/kern.opt.s <<'PY'
 import re, sys
 s = open(sys.argv[1]).read()
