@@ -124,7 +124,7 @@ def profile_rounds():
 
 def pmc_traffic(n, kernel, code):
     """HBM bytes per launch of this kernel at this batch size from the newest
-    committed PMC summary (tools/profile.sh -> tools/summarize_profile.py,
+    committed PMC summary (tools/gpu.sh profile -> tools/summarize_profile.py,
     profiles/rNN/pmc_traffic.json) that was measured on THIS build: its
     "build" entry's code hash must equal the loaded library's
     (fd_ed25519_gpu_build_id).  Returns (bytes or None, the file used or why
@@ -252,7 +252,8 @@ def hostfed_main(args):
     out["h2d_GBps"] = bw
     del d_buf, h_pin, h_page
     res = {}
-    for cfg, n, msg_sz in ((2, 65536, 200), (3, 1 << 20, None)):
+    want = [int(c) for c in os.environ.get("FD_HOSTFED_CONFIGS", "2,3").split(",")]
+    for cfg, n, msg_sz in [c for c in ((2, 65536, 200), (3, 1 << 20, None)) if c[0] in want]:
         arena, desc, sz, expect, data_desc = build_workload(n, msg_sz, seed=0, n_keys=min(n, 65536))
         g = fa.Ed25519Gpu(device_mask=1, max_batch=min(n, 65536))
         r = {"workload": data_desc, "bytes_per_verify": (sz + 17 * n) / n}
@@ -298,7 +299,7 @@ def hostfed_main(args):
         g.close()
         res["config%d" % cfg] = r
     out["configs"] = res
-    out["value"] = res["config2"]["submit_poll_registered"]
+    out["value"] = res["config2"]["submit_poll_registered"] if "config2" in res else None
     out["note"] = ("value: config 2 through submit/poll from a page-locked arena; the headline line's value is "
                    "device-resident.  link_bound = pinned H2D GB/s / bytes_per_verify")
     print(json.dumps(out), flush=True)
@@ -511,17 +512,14 @@ def main():
     d_outs = [d_out, torch.zeros(n, dtype=torch.int8, device=dev)]
     nstep = [0]
 
-    # a pipelined step over more than one wave per SIMD (config 3) is a run of
-    # pipe launches over chunks of pair_max descriptors (each launch one chunk
-    # of work, three chunks in flight across launches and across steps)
-    chunks = [(o, min(pair_max, n - o)) for o in range(0, n, pair_max)]
-
     def step():
-        if pipe:   # step i's codes land in d_outs[i % 2] once the launches two chunks later complete
+        # pipelined: step i's codes land in d_outs[i % 2] once the launches two
+        # chunks later complete; a batch above one wave per SIMD (config 3) is
+        # the library's k pre-pass + one launch per pair_max chunk, three chunks
+        # in flight across launches and across steps
+        if pipe:
             out = d_outs[nstep[0] & 1]
-            for o, c in chunks:
-                g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr() + 16 * o, c, out.data_ptr() + o,
-                           stream=stream.cuda_stream)
+            g.pipe_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, out.data_ptr(), stream=stream.cuda_stream)
             nstep[0] += 1
             return
         g.verify_batch_dev(d_arena.data_ptr(), sz, d_desc.data_ptr(), n, d_out.data_ptr(),
@@ -550,17 +548,29 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # the timed region: K steps back to back, one HIP event pair around all of
+    # them on the launch stream (an event record between launches costs the
+    # GPU 3-4 us, tools/marker_probe.py: none inside the region)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        ev[i][0].record(stream)
         step()
-        ev[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    region_ms = ev0.elapsed_time(ev1) / args.steps    # average launch duration over the region, gaps included
+    # after the region (untimed): each launch alone between two events, for
+    # the kernel's own duration (kernel_ms, kernel_frac)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(min(args.steps, 50))]
+    for a, b in ev:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     drain = settle()
 
@@ -604,8 +614,12 @@ def main():
                          "unit": "T MAC/s (32x32->64 multiply-adds, W=%.4g per verify)" % W_MAC,
                          "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
                          "priced_on": "ms_per_step (wall clock per step, per GPU: W x value / n_gpus)",
+                         "region_ms_per_launch": region_ms,
+                         "region_ms_note": "HIP events on the launch stream around the timed region / steps: the "
+                                           "average launch duration, inter-launch gaps included",
                          "kernel_ms": launch_ms, "kernel_frac": kernel_achieved / peak,
-                         "kernel_frac_note": "the same W priced on the mean event-bracketed launch (no inter-launch gap)"},
+                         "kernel_frac_note": "the same W priced on the mean event-bracketed launch (no inter-launch "
+                                             "gap), measured over up to 50 launches right after the timed region"},
             "cpu_baseline": None,
             "warmup_detail": {"prime_steps": prime, "prime_ms": args.prime_ms, "warmup_steps": args.warmup,
                               "untimed_steps_total": prime + args.warmup,

@@ -132,6 +132,8 @@ struct pipe_args {
      fd_ed25519_verify_batch_single_msg's precedence -- first phase-1 error
      by index, else ERR_MSG, else SUCCESS -- and the frag's last descriptor
      to finish writes the frag's record straight to the host */
+  uint32_t const *          kpre;       /* phase A: k = SHA-512(R || A || M) mod l of descriptor i at kpre[8 i]
+                                           (fd_ed25519_kpre_kernel ran over the batch; NULL: phase A hashes) */
   uint32_t const *          first_a;    /* phase A's batch is a frag batch: its frags' first descriptor indices */
   uint64_t *                fold_c;     /* phase C's batch's fold words (FD_FOLD_*; NULL: not a frag batch) */
   uint64_t const *          ftag_c;     /* its frags' tags */
@@ -259,6 +261,21 @@ struct shred_root_args {
    message). */
 #define FD_LEN_NB         16
 #define FD_LEN_SEG        16384
+/* k = SHA-512(R || A || M) mod l for a whole batch ahead of the pipelined
+   kernel (fd_ed25519_kpre_kernel, batches above one wave per SIMD: config 3's
+   1M variable-length messages), so phase A, which hashes otherwise, is short
+   and uniform: lane i takes descriptor idx[i] (the length order of
+   fd_len_sort_kernel; NULL: i) and writes k[8 di .. 8 di + 7]. */
+struct kpre_args {
+  uint8_t const *           arena;
+  uint64_t                  arena_sz;
+  fd_ed25519_desc_t const * desc;
+  uint64_t                  n;
+  uint32_t const *          idx;
+  uint32_t *                k;
+};
+#define FD_KERN_KPRE     "fd_ed25519_kpre_kernel"
+
 struct len_args {
   fd_ed25519_desc_t const * desc;
   uint64_t                  n;

@@ -504,9 +504,15 @@ __device__ __forceinline__ void verify_prep_scalars( uint32_t u[ 8 ], uint32_t v
 #ifdef FD_PHASE_STAMPS
                                                      , uint64_t * _st
 #endif
+                                                     , uint32_t const * krow = nullptr   /* k precomputed (wave-uniform) */
                                                      ) {
   uint32_t k[ 8 ];
-  hash_ram<FASTBLK>( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );
+  if( krow ) {
+    uint4 k0 = ((uint4 const *)krow)[0], k1 = ((uint4 const *)krow)[1];
+    k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w; k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
+  } else {
+    hash_ram<FASTBLK>( k, sig, pub, args.arena, d.msg_off, d.msg_sz, lim_dw );
+  }
   FE_FENCE();
   STAMP( 2 );
   lat_short_vector( k, u, v, un );
@@ -848,7 +854,7 @@ __device__ __forceinline__ int comb_lds_eq( ge_p3 & acc, uint4 * buf, uint32_t c
   int d = FD_WDIG( 0 );
   ctab_fetch_lds( buf, ctab, 0, d );
 #pragma unroll 1
-  for( int k=0; k<FD_CTAB_POS-1; k++ ) {
+  for( int k=0; k<FD_COMB_POS_RUN-1; k++ ) {       /* (FD_COMB_POS_RUN: fd_diag.h) */
     ge_precomp bp;
     {
       dma_wait();
@@ -861,7 +867,7 @@ __device__ __forceinline__ int comb_lds_eq( ge_p3 & acc, uint4 * buf, uint32_t c
       d = dn;
     }
     FE_FENCE();
-    ge_madd( acc, acc, bp, k + 2 < FD_CTAB_POS );
+    ge_madd( acc, acc, bp, k + 2 < FD_COMB_POS_RUN );
     FE_FENCE();
   }
 #undef FD_WDIG
@@ -1323,7 +1329,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #ifdef FD_PHASE_STAMPS
                                     , nullptr
 #endif
-                                    );
+                                    , a.kpre ? a.kpre + 8u*di : nullptr );
     FE_FENCE();
     int P = wave_top_pos( nbits );                  /* the chain's doublings (ybias_p) */
     if( valid ) {
@@ -1750,6 +1756,39 @@ fd_len_sort_kernel( len_args a ) {
   for( uint32_t j=tid; j<m; j+=1024u ) {
     uint32_t o = atomicAdd( &cur[ len_bucket( a.desc[ lo + j ] ) ], 1u );
     a.idx[ lo + o ] = (uint32_t)(lo + j);
+  }
+}
+
+/* k = SHA-512(R || A || M) mod l ahead of the pipelined kernel (kpre_args,
+   fd_ed25519_gpu_abi.h): lane i hashes descriptor idx[i] (length order, so a
+   wave's messages have similar block counts) with the one-shot kernels'
+   hash (message fetched a block ahead, interior blocks without padding
+   masks) and stores k at k[8 di].  Descriptors outside the arena get no
+   hash (phase A never reads their k). */
+extern "C" __global__ void __launch_bounds__( 256 )
+fd_ed25519_kpre_kernel( kpre_args a ) {
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if( (i & ~(uint64_t)63) >= a.n ) return;                      /* whole waves past n */
+  bool valid = i < a.n;
+  uint64_t di = valid ? (a.idx ? (uint64_t)a.idx[ i ] : i) : 0u;
+  fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
+  if( valid ) d = a.desc[ di ];
+  uint64_t asz = a.arena_sz;
+  bool ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
+            (uint64_t)d.msg_off + d.msg_sz <= asz;
+  uint32_t lim_dw = (uint32_t)((asz + 3u) >> 2) + 1u;
+  uint32_t R[ 8 ], A[ 8 ], k[ 8 ];
+#pragma unroll
+  for( int j=0; j<8; j++ ) { R[j] = 0u; A[j] = 0u; k[j] = 0u; }
+  if( ok ) {
+    load_words<8>( R, a.arena, d.sig_off, lim_dw );
+    load_words<8>( A, a.arena, d.pub_off, lim_dw );
+  }
+  if( !ok ) d.msg_sz = 0u;                                         /* (every lane takes part in the wave's loop) */
+  hash_ram<true>( k, R, A, a.arena, d.msg_off, d.msg_sz, lim_dw );
+  if( ok ) {
+    uint4 * o = (uint4 *)(a.k + 8u*di);
+    o[0] = make_uint4( k[0], k[1], k[2], k[3] ); o[1] = make_uint4( k[4], k[5], k[6], k[7] );
   }
 }
 

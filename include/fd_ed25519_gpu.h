@@ -215,6 +215,12 @@ int fd_ed25519_verify_batch_gpu_dev( fd_ed25519_gpu_t * ctx, int dev_idx,
    64-signature wave per SIMD; the three phases give every SIMD three waves.
    desc_cnt == 0 is a drain step.  desc_cnt <= the context's max_batch
    (rounded up to 256); a context with hot keys cached is refused (ERR_ARG).
+   A batch above one wave per SIMD (256 x CUs signatures) is several
+   launches: k = SHA-512(R || A || M) mod l of the whole batch first (in
+   message-length order), then one pipelined launch per 256 x CUs chunk whose
+   phase A reads its k instead of hashing; its d_arena / d_desc must stay
+   valid until the call's last chunk launch has completed, and its codes are
+   final two calls (or a flush) later like any batch's.
    Codes are the same as every other entry point's.  Replaces nothing in the
    reference: the verify tile's fd_txn_verify calls (fd_verify.h:43-88) see
    the same codes, one batch later. */

@@ -112,3 +112,27 @@ def test_pipe_refuses_oversize_and_hot_keys(gpu):
             gpu.pipe_dev(a[0].data_ptr(), a[2], a[1].data_ptr(), a[3], a[4].data_ptr())
     finally:
         gpu.keycache_clear()
+
+
+@pytest.mark.parametrize("flavour,key", [(fa.CODES_AVX512, "code"), (fa.CODES_REF, "code_ref")])
+def test_pipe_big_batches_kpre(flavour, key):
+    """Batches above one wave per SIMD through pipe_dev (config 3's form):
+    k = SHA-512(R||A||M) mod l for the whole batch in message-length order
+    (fd_ed25519_kpre_kernel), then 64K chunks whose phase A reads k; every
+    golden record (variable-length messages 0..1232 B, adversarial classes)
+    tiled to 140K in random order, then 70K, then 5 -- codes bit-exact with
+    the reference's across the calls and the flush."""
+    recs = _golden()
+    rng = np.random.default_rng(77)
+    g = fa.Ed25519Gpu(device_mask=1, max_batch=160000)
+    try:
+        sets = [[recs[i % len(recs)] for i in rng.permutation(140000)],
+                [recs[i % len(recs)] for i in rng.permutation(70000)], recs[7:12]]
+        batches = [_dev(s) for s in sets]
+        st = torch.cuda.Stream()
+        g.set_codes(flavour)
+        _run_pipe(g, batches, st)
+    finally:
+        g.close()
+    for s, b in zip(sets, batches):
+        assert np.array_equal(b[4].cpu().numpy(), np.array([r[key] for r in s], np.int8))

@@ -592,7 +592,7 @@ def test_stage_frag_areas_freed_between_batches(gpu):
     ast = fa.AsyncStage(gpu, fa.TCache(), 64, threads=1, device_parse=True)
     try:
         for rnd in range(3):
-            names = ["valid_txn_1sig", "valid_txn_2sigs", "invalid_txn_2sigs"]
+            names = ["valid_txn_2sigs", "invalid_txn_same_1sig", "valid_txn_1sig"]   # :219-264's F-then-S pair
             arena, frags = _mk_frags([fx[k] for k in names])
             arena = arena.copy()
             res = np.zeros(len(frags), np.int8); sig = np.zeros(len(frags), np.uint64)
@@ -600,7 +600,7 @@ def test_stage_frag_areas_freed_between_batches(gpu):
             ast.submit(arena, len(arena), np.ascontiguousarray(frags), res, sig)
             while ast.pending():
                 ast.poll(True)
-            assert list(res) == [S, S, F], (rnd, list(res))
+            assert list(res) == [S, F, S], (rnd, list(res))
             gpu.host_register(arena)          # fails with AlreadyRegistered if the stage had kept it
             gpu.host_unregister(arena)
             del arena, frags

@@ -9,10 +9,15 @@
 #   tools/gpu.sh bytes A.so B.so ...    per build: FETCH_SIZE, WRITE_SIZE and GRBM/SQ passes over
 #                                       steady-state pipe launches -> gpurun_out/bytes_$TAG.jsonl
 #   tools/gpu.sh bench [bench args]     one bench.py line -> gpurun_out/bench_$TAG.json
-#   tools/gpu.sh profile [bench args]   kernel trace + PMC set of bench.py -> gpurun_out/prof_$TAG/
+#   tools/gpu.sh profile [bench args]   bench lines, kernel trace + PMC set of bench.py -> gpurun_out/prof_$TAG/
+#                                       (then tools/summarize_profile.py gpurun_out/prof_$TAG profiles/rNN)
+#   tools/gpu.sh offload                the two-process offload link run (server + client)
 #   tools/gpu.sh stage [args]           verify-stage bench (tools/bench_verify_stage.py; default 1M frags)
 #   tools/gpu.sh stagetrace             kernel + copy trace of the stage bench -> gpurun_out/stagetr_$TAG/
 #   tools/gpu.sh hostfedtrace           kernel + copy trace of bench.py --path host-fed (+ the process's maps at exit)
+#   tools/gpu.sh abstage "A:" "B:ENV=v" same-process A/B of stage settings (tools/ab_stage.py)
+#   tools/gpu.sh clock 2|3              in-kernel clock stamps of config 2 / 3 (stamps build)
+#   tools/gpu.sh crashctl MODE          exit-SIGSEGV control run (tools/crash_control.py) under the trace flags
 #   tools/gpu.sh run SECONDS CMD...     any other command under its own time limit
 set -e
 mkdir -p gpurun_out
@@ -44,16 +49,20 @@ case "$cmd" in
       || { tail -20 gpurun_out/bench_$T.err; exit 1; }
     cat gpurun_out/bench_$T.json ;;
   profile)
+    # the layout tools/summarize_profile.py reads; the kernel trace runs 2,000 timed steps so its
+    # --stats average is the steady state (the prime / warm-up launches at a ramping clock are few)
     cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
     o=gpurun_out/prof_$T; mkdir -p $o
-    timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $o/kt -o kt -- python3 bench.py --no-cpu "$@" \
-      > $o/kt_bench.json 2> $o/kt.err
-    for pass in "FETCH_SIZE" "WRITE_SIZE" \
-                "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_ANY" \
-                "SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES SQ_THREAD_CYCLES_VALU" \
-                "GRBM_GUI_ACTIVE GRBM_COUNT"; do
-      p=${pass%% *}
-      timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d $o/pmc_$p -o pmc -- \
+    timeout -k 10 300 python3 bench.py "$@" > $o/bench.json 2> $o/bench.err
+    timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 "$@" > $o/bench_driver_form.json 2> $o/bench_driver_form.err
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/kt -o kt -- \
+      python3 bench.py --no-cpu --steps 2000 --warmup 50 "$@" > $o/kt_bench.json 2> $o/kt.err
+    for pass in "fetch FETCH_SIZE" "write WRITE_SIZE" \
+                "sq SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_ANY" \
+                "issue SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_ANY" \
+                "grbm GRBM_GUI_ACTIVE GRBM_COUNT"; do
+      p=${pass%% *}; c=${pass#* }
+      timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $o/pmc_$p -o pmc -- \
         python3 bench.py --no-cpu --steps 20 --warmup 5 "$@" > /dev/null 2> $o/pmc_$p.err
     done
     echo done > $o/DONE ;;
@@ -72,6 +81,31 @@ case "$cmd" in
       --output-format csv -d gpurun_out/hostfedtr_$T -o tr -- python3 bench.py --path host-fed \
       > gpurun_out/hostfedtr_$T.json 2> gpurun_out/hostfedtr_$T.err || { tail -30 gpurun_out/hostfedtr_$T.err; exit 1; }
     cat gpurun_out/hostfedtr_$T.json ;;
+  offload)
+    # the server (owns the GPU) in the background, the client (no GPU) in front
+    NAME=/fdvo_e2e_$$
+    timeout -k 10 300 ./firedancer_amd/fd_verify_offload_server --name $NAME --batch ${BATCH:-65536} --threads ${THREADS:-16} \
+      > gpurun_out/offload_server_$T.json 2> gpurun_out/offload_server_$T.err &
+    SRV=$!
+    for i in $(seq 600); do grep -q ready gpurun_out/offload_server_$T.json 2>/dev/null && break; kill -0 $SRV 2>/dev/null || break; sleep 0.2; done
+    timeout -k 10 240 python3 tools/bench_offload.py --name $NAME ${CLIENT_ARGS} > gpurun_out/offload_client_$T.json \
+      2> gpurun_out/offload_client_$T.err || { kill $SRV; wait $SRV; exit 1; }
+    wait $SRV
+    cat gpurun_out/offload_client_$T.json gpurun_out/offload_server_$T.json ;;
+  clock)
+    # in-kernel clock stamps (stamps build) for bench config $1 (2: pipe kernel, 3: single-lane kernel)
+    FD_ED25519_GPU_LIB=tools/bin/libfd_ed25519_gpu_stamps.so timeout -k 10 300 python3 tools/clock_stamps.py --config $1 \
+      > gpurun_out/clock_c$1_$T.json 2> gpurun_out/clock_c$1_$T.err || { tail -20 gpurun_out/clock_c$1_$T.err; exit 1; }
+    cat gpurun_out/clock_c$1_$T.json ;;
+  crashctl)
+    # the exit-time SIGSEGV control (tools/crash_control.py MODE) under the host-fed trace's profiler flags
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+    FD_MAPS_OUT=gpurun_out/crashctl_$1_maps.txt timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+      --output-format csv -d gpurun_out/crashctl_$1 -o tr -- python3 tools/crash_control.py $1 \
+      > gpurun_out/crashctl_$1.out 2> gpurun_out/crashctl_$1.err; echo "crashctl $1 rc=$?"; tail -3 gpurun_out/crashctl_$1.err ;;
+  abstage)
+    timeout -k 10 600 python3 -u tools/ab_stage.py "$@" > gpurun_out/abstage_$T.log 2>&1 || { tail -20 gpurun_out/abstage_$T.log; exit 1; }
+    grep -v amdgpu.ids gpurun_out/abstage_$T.log ;;
   run)
     lim=$1; shift
     timeout -k 10 $lim "$@" ;;
