@@ -228,31 +228,42 @@ def hostfed_main(args):
     from a pageable and from a page-locked arena; bytes per verify (the
     arena bytes the descriptors touch + the 16-B descriptor + the 1-B code)
     and the link-bound ceiling they imply."""
-    import torch
+    # No torch here: the library and the HIP runtime it links are the process's
+    # only GPU stack (torch's wheel bundles a second HIP / HSA runtime; with
+    # both loaded, rocprofv3's finalizer faulted at exit, DESIGN.md §9).
+    os.environ["FD_ED25519_GPU_NO_TORCH"] = "1"
     import firedancer_amd as fa
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
     out = {"metric": "host-fed Ed25519 verifies/sec (PCIe in the loop)", "unit": "verifies/s", "n_gpus": 1,
            "data": "synthetic (tools/synth.py), all valid"}
-    # H2D bandwidth
+    # H2D bandwidth: 256 MB from page-locked (async copies) and from pageable memory
+    g0 = fa.Ed25519Gpu(device_mask=1, max_batch=1)       # loads the library (and its HIP runtime) first
+    hip = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
     nb = 256 << 20
-    h_pin = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h_pin, d_buf = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipSetDevice(0) == 0
+    assert hip.hipHostMalloc(ctypes.byref(h_pin), ctypes.c_size_t(nb), 0) == 0
+    assert hip.hipMalloc(ctypes.byref(d_buf), ctypes.c_size_t(nb)) == 0
     h_page = np.ones(nb, np.uint8)
-    d_buf = torch.empty(nb, dtype=torch.uint8, device=dev)
     bw = {}
-    for name, src in (("pinned", h_pin), ("pageable", torch.from_numpy(h_page))):
-        for _ in range(2):
-            d_buf.copy_(src, non_blocking=(name == "pinned"))
-        torch.cuda.synchronize()
+    for name, src in (("pinned", h_pin.value), ("pageable", h_page.ctypes.data)):
+        def copies(k):
+            for _ in range(k):
+                if name == "pinned":
+                    assert hip.hipMemcpyAsync(d_buf, ctypes.c_void_p(src), ctypes.c_size_t(nb), 1, None) == 0
+                else:
+                    assert hip.hipMemcpy(d_buf, ctypes.c_void_p(src), ctypes.c_size_t(nb), 1) == 0
+            assert hip.hipDeviceSynchronize() == 0
+        copies(2)
         t = time.perf_counter()
-        for _ in range(8):
-            d_buf.copy_(src, non_blocking=(name == "pinned"))
-        torch.cuda.synchronize()
+        copies(8)
         bw[name] = 8 * nb / (time.perf_counter() - t) / 1e9
     out["h2d_GBps"] = bw
-    del d_buf, h_pin, h_page
+    hip.hipFree(d_buf)
+    hip.hipHostFree(h_pin)
+    del h_page
     res = {}
     want = [int(c) for c in os.environ.get("FD_HOSTFED_CONFIGS", "2,3").split(",")]
+    skip = os.environ.get("FD_HOSTFED_SKIP", "").split(",")    # dev: sections left out (exit-crash bisection)
     for cfg, n, msg_sz in [c for c in ((2, 65536, 200), (3, 1 << 20, None)) if c[0] in want]:
         arena, desc, sz, expect, data_desc = build_workload(n, msg_sz, seed=0, n_keys=min(n, 65536))
         g = fa.Ed25519Gpu(device_mask=1, max_batch=min(n, 65536))
@@ -285,19 +296,24 @@ def hostfed_main(args):
             dt = time.perf_counter() - t0
             assert all(np.array_equal(o, expect[i:i + c]) for (i, c, o) in todo)
             return len(todo) and sum(c for _, c, _ in todo) / dt
-        stream()
+        if "warm" not in skip:
+            stream()
         r["submit_poll_pageable"] = stream()
         g.host_register(arena)
-        stream()
-        g.host_stats(reset=True)
+        if "warm" not in skip:
+            stream()
+        if "stats" not in skip:
+            g.host_stats(reset=True)
         r["submit_poll_registered"] = stream()
-        hs = g.host_stats()
-        r["submit_path_ms_registered"] = {k[:-3]: v / 1e6 for k, v in hs.items() if k.endswith("_ns")}
-        r["h2d_bytes_per_verify_registered"] = hs["h2d_bytes"] / (n * reps)
+        if "stats" not in skip:
+            hs = g.host_stats()
+            r["submit_path_ms_registered"] = {k[:-3]: v / 1e6 for k, v in hs.items() if k.endswith("_ns")}
+            r["h2d_bytes_per_verify_registered"] = hs["h2d_bytes"] / (n * reps)
         g.host_unregister(arena)
         r["link_bound_verifies_per_s_pinned"] = bw["pinned"] * 1e9 / r["bytes_per_verify"]
         g.close()
         res["config%d" % cfg] = r
+    g0.close()
     out["configs"] = res
     out["value"] = res["config2"]["submit_poll_registered"] if "config2" in res else None
     out["note"] = ("value: config 2 through submit/poll from a page-locked arena; the headline line's value is "

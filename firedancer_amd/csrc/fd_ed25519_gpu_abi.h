@@ -90,6 +90,36 @@ struct verify_args {
    16-byte record, written by the device with one store. */
 typedef struct __attribute__(( aligned( 16 ) )) { uint32_t tag_lo, tag_hi; int32_t status; uint32_t pad; } fd_frec_t;
 
+/* Device-side frag parsing (verify stage, fd_verify_stage.cpp): the frags
+   [off, off+sz) index a copy of the arena span [span_lo, span_lo+span_sz).
+   One launch parses every frag and writes its descriptors at their final
+   positions (a single-pass scan of the per-frag signature counts with
+   decoupled look-back across workgroups, flag words tagged with the batch's
+   epoch so they need no reset). */
+struct fparse_args {
+  uint8_t const *                span;       /* device copy of arena[span_lo, span_lo + span_sz) */
+  uint64_t                       span_sz;
+  uint64_t                       span_lo;
+  uint32_t                       host_parity; /* (uintptr_t)host_arena & 1: the tile aligns host addresses */
+  uint32_t                       epoch;      /* this batch's look-back epoch (nonzero, new per batch of the slot) */
+  uint64_t                       arena_sz;   /* the host arena's size (frags beyond it are BAD) */
+  fd_ed25519_gpu_frag_t const *  frag;
+  uint64_t                       n;
+  int8_t *                       status;     /* out: 0 / FD_TXN_VERIFY_FAILED / _BAD_FRAG; 0s become the folded code */
+  uint64_t *                     tag;        /* out */
+  uint32_t *                     first;      /* out: the frag's first descriptor index */
+  uint64_t *                     fold;       /* out: the fold word (FD_FOLD_SH), set to the descriptor count */
+  uint64_t *                     flag;       /* look-back words, one per workgroup (zeroed once at allocation) */
+  uint32_t *                     total;      /* out: descriptor count */
+  uint32_t *                     err;        /* host-mapped: 1 if a look-back wait expired (the batch fails) */
+  fd_ed25519_desc_t *            desc;       /* out: descriptors */
+  uint64_t                       desc_cap;
+  int8_t const *                 code;       /* fold kernel (one-shot verify): per-descriptor codes */
+  fd_frec_t *                    hrec;       /* page-locked host staging, one {tag lo, tag hi, status, 0} per frag
+                                                (device-mapped): the parse writes frags without descriptors, the
+                                                pipelined kernel's phase C or the fold kernel the others */
+};
+
 #define FD_PH_R           0            /* R's encoding, 8 words                        */
 #define FD_PH_YU          8            /* u + 8 (16^0 + ... + 16^(nw-2)), 8 words      */
 #define FD_PH_YV          16           /* v + the same bias, 8 words                   */
@@ -138,6 +168,11 @@ struct pipe_args {
   uint64_t *                fold_c;     /* phase C's batch's fold words (FD_FOLD_*; NULL: not a frag batch) */
   uint64_t const *          ftag_c;     /* its frags' tags */
   fd_frec_t *               frec_c;     /* its page-locked staging records (device-mapped) */
+  /* in-launch parse (frag batches): nonzero = gp, the workgroups whose phase-A
+     waves parse the batch's frags (fp) before phase A reads the descriptors
+     (v.cnt unused); 0: the descriptors came from an earlier launch */
+  uint64_t                  aparse;
+  fparse_args               fp;
 };
 /* A frag's fold word (64 bits, set to its descriptor count by the parse):
    each descriptor k < 16 of the frag adds, in ONE relaxed atomic, its code
@@ -162,36 +197,6 @@ struct kpart_args {
   uint32_t *                miss_idx;
   uint32_t *                counts;    /* [0] hits, [1] misses (zeroed before launch) */
   uint32_t const *          ncnt;      /* if set: the batch is desc[0, min(n, *ncnt)) */
-};
-
-/* Device-side frag parsing (verify stage, fd_verify_stage.cpp): the frags
-   [off, off+sz) index a copy of the arena span [span_lo, span_lo+span_sz).
-   One launch parses every frag and writes its descriptors at their final
-   positions (a single-pass scan of the per-frag signature counts with
-   decoupled look-back across workgroups, flag words tagged with the batch's
-   epoch so they need no reset). */
-struct fparse_args {
-  uint8_t const *                span;       /* device copy of arena[span_lo, span_lo + span_sz) */
-  uint64_t                       span_sz;
-  uint64_t                       span_lo;
-  uint32_t                       host_parity; /* (uintptr_t)host_arena & 1: the tile aligns host addresses */
-  uint32_t                       epoch;      /* this batch's look-back epoch (nonzero, new per batch of the slot) */
-  uint64_t                       arena_sz;   /* the host arena's size (frags beyond it are BAD) */
-  fd_ed25519_gpu_frag_t const *  frag;
-  uint64_t                       n;
-  int8_t *                       status;     /* out: 0 / FD_TXN_VERIFY_FAILED / _BAD_FRAG; 0s become the folded code */
-  uint64_t *                     tag;        /* out */
-  uint32_t *                     first;      /* out: the frag's first descriptor index */
-  uint64_t *                     fold;       /* out: the fold word (FD_FOLD_SH), set to the descriptor count */
-  uint64_t *                     flag;       /* look-back words, one per workgroup (zeroed once at allocation) */
-  uint32_t *                     total;      /* out: descriptor count */
-  uint32_t *                     err;        /* host-mapped: 1 if a look-back wait expired (the batch fails) */
-  fd_ed25519_desc_t *            desc;       /* out: descriptors */
-  uint64_t                       desc_cap;
-  int8_t const *                 code;       /* fold kernel (one-shot verify): per-descriptor codes */
-  fd_frec_t *                    hrec;       /* page-locked host staging, one {tag lo, tag hi, status, 0} per frag
-                                                (device-mapped): the parse writes frags without descriptors, the
-                                                pipelined kernel's phase C or the fold kernel the others */
 };
 
 /* Frags per workgroup of the parse and fold kernels. */

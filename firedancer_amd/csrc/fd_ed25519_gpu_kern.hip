@@ -1251,12 +1251,17 @@ __device__ __forceinline__ void hand_to_lds( uint32_t * y, uint32_t const * hand
   for( int j=0; j<24; j++ ) if( j < nwords ) y[ j*64 + lane ] = t[j];
 }
 
+__device__ __forceinline__ uint32_t pipe_aparse( fparse_args const & a, uint64_t gp, uint32_t * s_ap, int wv, int lane );
+__device__ __forceinline__ fd_ed25519_desc_t desc_ld_coh( fd_ed25519_desc_t const * p );
+
 extern "C" __global__ void __launch_bounds__( 3 * FD_VERIFY_BLOCK, 1 )
 fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   __shared__ uint4    s_buf[ 2 ][ 4 ][ 10*64 ];       /* phase C / B: a table entry per wave      */
   __shared__ uint32_t s_y[ 2 ][ 4 ][ 24*64 ];         /* phase C / B: u, v, w digit scalars       */
   __shared__ uint32_t s_lo[ 4*FD_LEN_NB + FD_VERIFY_BLOCK + 2 ];   /* phase A: length order (pipe_len_order) */
+  __shared__ uint32_t s_ap[ 8 ];                                    /* phase A: in-launch parse (pipe_aparse) */
   if( threadIdx.x < 2 ) s_lo[ 4*FD_LEN_NB + FD_VERIFY_BLOCK + threadIdx.x ] = 0u;
+  if( threadIdx.x < 8 ) s_ap[ threadIdx.x ] = 0u;
   __syncthreads();
   /* 0: phase C, 1: phase B, 2: phase A -- the thirds' waves are created in
      this order and the SIMD's arbiter favours the oldest (the other five
@@ -1293,10 +1298,12 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   if( role == 2 ) {
     /* ---- phase A, batch j ---- */
     uint64_t nn = args.n;                                               /* args.cnt: a device-side count <= n */
-    if( args.cnt ) nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)*args.cnt ) );
+    if( a.aparse )                   /* the batch's frags parsed in this launch: the count this workgroup may use */
+      nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)pipe_aparse( a.fp, a.aparse, s_ap, wv, lane ) ) );
+    else if( args.cnt ) nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)*args.cnt ) );
     uint64_t b0 = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK, di = gid;   /* di: the descriptor this lane verifies */
     if( a.lsort && b0 + FD_VERIFY_BLOCK <= nn )                       /* full workgroups only: all four waves here */
-      di = b0 + pipe_len_order( len_bucket( args.desc[ gid ] ), wv, lane, s_lo, s_lo + 4*FD_LEN_NB,
+      di = b0 + pipe_len_order( len_bucket( a.aparse ? desc_ld_coh( args.desc + gid ) : args.desc[ gid ] ), wv, lane, s_lo, s_lo + 4*FD_LEN_NB,
                                 s_lo + 4*FD_LEN_NB + FD_VERIFY_BLOCK,
                                 a.err ? a.err + (a.seq % FD_PIPE_ERR_RING) : nullptr, (uint32_t)a.seq + 1u );
     if( (gid & ~(uint64_t)63) >= nn ) {
@@ -1305,7 +1312,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
     }
     bool valid = gid < nn;
     fd_ed25519_desc_t d; d.sig_off = 0u; d.pub_off = 0u; d.msg_off = 0u; d.msg_sz = 0u; d.txn_idx = 0u;
-    if( valid ) d = args.desc[ di ];
+    if( valid ) d = a.aparse ? desc_ld_coh( args.desc + di ) : args.desc[ di ];
     uint64_t asz = args.arena_sz;
     bool desc_ok = valid && (uint64_t)d.sig_off + 64u <= asz && (uint64_t)d.pub_off + 32u <= asz &&
                    (uint64_t)d.msg_off + d.msg_sz <= asz;
@@ -1349,7 +1356,11 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #pragma unroll
       for( int j=0; j<8; j++ ) h[ (uint64_t)(FD_PH_A + j)*cap ] = pub[j];
       h[ (uint64_t)FD_PH_IDX*cap ] = (uint32_t)di;
-      if( a.first_a ) h[ (uint64_t)FD_PH_FRAG*cap ] = (uint32_t)d.txn_idx | ((uint32_t)(di - a.first_a[ d.txn_idx ]) << 16);
+      if( a.first_a ) {
+        uint32_t f0 = a.aparse ? __hip_atomic_load( (uint32_t *)a.first_a + d.txn_idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT )
+                               : a.first_a[ d.txn_idx ];
+        h[ (uint64_t)FD_PH_FRAG*cap ] = (uint32_t)d.txn_idx | ((uint32_t)(di - f0) << 16);
+      }
     }
     if( lane == 0 ) a.nw_a[ gid >> 6 ] = (uint8_t)P;     /* the wave's top-digit position */
     FE_FENCE();
@@ -1965,7 +1976,7 @@ __device__ __forceinline__ uint32_t frag_lookback( uint64_t * flag, uint64_t t, 
     uint64_t w = k >= 0 ? __hip_atomic_load( flag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) : (ep | (FD_LB_PREFIX << 30));
     uint64_t stt = (w >> 30) & 3ull;
     bool ready = (w & 0xffffffff00000000ull) == ep && stt != 0ull;
-    uint64_t pre = __ballot( ready && stt == FD_LB_PREFIX );
+    uint64_t pre = __ballot( ready && stt >= FD_LB_PREFIX );   /* FD_LB_DONE (in-launch parse) is a prefix too */
     uint64_t need = pre ? ((pre & (~pre + 1ull)) << 1) - 1ull : ~0ull;   /* lanes up to the nearest prefix */
     if( __ballot( !ready ) & need ) {
       if( ++spin > FD_LB_SPIN ) { *late = 1; break; }
@@ -1996,6 +2007,80 @@ __device__ __forceinline__ uint32_t frag_lookback( uint64_t * flag, uint64_t t, 
    base + its exclusive count; the last tile writes the batch's total.  Per
    frag: status, tag, first descriptor index, and the fold words (min key
    ~0, the descriptor count) the phase-C fold counts down. */
+/* One frag's checks and fields (frag i of the batch; i >= n: BAD_FRAG, no
+   descriptors): status, tag, signature count and the descriptor fields. */
+struct frag_fields { int st; uint64_t tag; uint32_t cnt, so, po, mo, ms; };
+__device__ __forceinline__ frag_fields frag_parse_one( fparse_args const & a, uint64_t i ) {
+  frag_fields r; r.st = FD_TXN_VERIFY_BAD_FRAG; r.tag = 0u; r.cnt = 0u; r.so = 0u; r.po = 0u; r.mo = 0u; r.ms = 0u;
+  fd_ed25519_gpu_frag_t f; f.off = 0xffffffffu; f.sz = 0u;
+  if( i < a.n ) f = a.frag[ i ];
+  uint64_t off = f.off, sz = f.sz;
+  do {
+    if( off > a.arena_sz || sz > a.arena_sz - off || sz < 2u ) break;          /* fd_verify.c:94-96 */
+    if( off < a.span_lo || off + sz > a.span_lo + a.span_sz ) break;
+    uint64_t ro = off - a.span_lo, re = ro + sz;                                /* the frag, span-relative */
+    uint64_t psz = span_ld16( a.span + re - 2u );                               /* :98 */
+    if( psz > 2086u ) break;                                                    /* :101-103 */
+    uint64_t t = ro + psz + ((a.host_parity + off + psz) & 1u);                  /* :108 align_up( addr, 2 ) */
+    if( t + 14u > re ) break;                    /* every field read lies inside the frag (fd_txn_parse output does) */
+    uint8_t const * txn = a.span + t;
+    if( span_ld16( txn + 12 ) >= psz ) break;                                   /* :112-115 */
+    uint64_t c = txn[1];
+    uint64_t s_ = ro + span_ld16( txn + 2 ), p_ = ro + span_ld16( txn + 10 ), m_ = span_ld16( txn + 4 );
+    if( s_ + 8u > re ) break;
+    uint8_t const * sg = a.span + s_;
+#pragma unroll
+    for( int b=7; b>=0; b-- ) r.tag = (r.tag << 8) | sg[b];
+    if( m_ > psz || psz > sz ) break;
+    if( !c || c > 16u ) { r.st = FD_TXN_VERIFY_FAILED; break; }                /* batch_sz 0 or > 16 -> ERR_SIG */
+    if( c * FD_FRAG_SIG_BYTES > sz ) break;                                     /* more signatures than the frag holds */
+    if( s_ + 64u*c > re || p_ + 32u*c > re ) break;
+    r.st = 0; r.cnt = (uint32_t)c; r.so = (uint32_t)s_; r.po = (uint32_t)p_; r.mo = (uint32_t)(ro + m_); r.ms = (uint32_t)(psz - m_);
+  } while( 0 );
+  return r;
+}
+
+/* Descriptor stores and loads that are coherent across the XCDs inside one
+   launch (agent-scope relaxed atomics: write-through stores, loads that do
+   not hit a stale L2 line), for the pipelined kernel's in-launch parse: its
+   phase-A waves read descriptors other workgroups -- on other XCDs, whose
+   L2s are not coherent with this one -- wrote in the same launch.  No fence
+   with a cache operation is needed: the data never sits dirty in an L2. */
+__device__ __forceinline__ void desc_st_coh( fd_ed25519_desc_t * p, fd_ed25519_desc_t const & d ) {
+  uint64_t lo = (uint64_t)d.sig_off | ((uint64_t)d.pub_off << 32);
+  uint64_t hi = (uint64_t)d.msg_off | ((uint64_t)d.msg_sz << 32) | ((uint64_t)d.txn_idx << 48);
+  __hip_atomic_store( (uint64_t *)p,     lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  __hip_atomic_store( (uint64_t *)p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+}
+__device__ __forceinline__ fd_ed25519_desc_t desc_ld_coh( fd_ed25519_desc_t const * p ) {
+  uint64_t lo = __hip_atomic_load( (uint64_t *)p,     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  uint64_t hi = __hip_atomic_load( (uint64_t *)p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  fd_ed25519_desc_t d;
+  d.sig_off = (uint32_t)lo; d.pub_off = (uint32_t)(lo >> 32);
+  d.msg_off = (uint32_t)hi; d.msg_sz = (uint16_t)(hi >> 32); d.txn_idx = (uint16_t)(hi >> 48);
+  return d;
+}
+
+/* Frag i's outputs: status, tag, first descriptor index, fold word, the
+   host record of a frag without descriptors, and its descriptors
+   (coherent stores for the in-launch parse). */
+template<bool COH>
+__device__ __forceinline__ void frag_write( fparse_args const & a, uint64_t i, frag_fields const & r, uint32_t first ) {
+  if( i >= a.n ) return;
+  a.status[ i ] = (int8_t)r.st; a.tag[ i ] = r.tag;
+  if( COH ) __hip_atomic_store( a.first + i, first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  else      a.first[ i ] = first;
+  a.fold[ i ] = r.cnt;
+  if( r.st ) ((uint4 *)a.hrec)[ i ] = make_uint4( (uint32_t)r.tag, (uint32_t)(r.tag >> 32), (uint32_t)(int32_t)r.st, 0u );   /* no descriptors: final */
+  for( uint32_t j=0; j<r.cnt && (uint64_t)first + j < a.desc_cap; j++ ) {
+    fd_ed25519_desc_t d;
+    d.sig_off = r.so + 64u*j; d.pub_off = r.po + 32u*j; d.msg_off = r.mo;
+    d.msg_sz = (uint16_t)r.ms; d.txn_idx = (uint16_t)i;
+    if( COH ) desc_st_coh( a.desc + first + j, d );
+    else      a.desc[ first + j ] = d;
+  }
+}
+
 extern "C" __global__ void __launch_bounds__( FD_FRAG_BLOCK )
 fd_frag_parse_kernel( fparse_args a ) {
   __shared__ uint32_t wsum[ FD_FRAG_BLOCK / 64u ];
@@ -2003,36 +2088,9 @@ fd_frag_parse_kernel( fparse_args a ) {
   uint64_t ntile = (a.n + FD_FRAG_BLOCK - 1u) / FD_FRAG_BLOCK;
   for( uint64_t tl=blockIdx.x; tl<ntile; tl+=gridDim.x ) {
     uint64_t i = tl * FD_FRAG_BLOCK + threadIdx.x;
-    fd_ed25519_gpu_frag_t f; f.off = 0xffffffffu; f.sz = 0u;
-    if( i < a.n ) f = a.frag[ i ];
-    int st = FD_TXN_VERIFY_BAD_FRAG;
-    uint64_t tag = 0u;
-    uint32_t cnt = 0u, so = 0u, po = 0u, mo = 0u, ms = 0u;
-    uint64_t off = f.off, sz = f.sz;
-    do {
-      if( off > a.arena_sz || sz > a.arena_sz - off || sz < 2u ) break;          /* fd_verify.c:94-96 */
-      if( off < a.span_lo || off + sz > a.span_lo + a.span_sz ) break;
-      uint64_t ro = off - a.span_lo, re = ro + sz;                                /* the frag, span-relative */
-      uint64_t psz = span_ld16( a.span + re - 2u );                               /* :98 */
-      if( psz > 2086u ) break;                                                    /* :101-103 */
-      uint64_t t = ro + psz + ((a.host_parity + off + psz) & 1u);                  /* :108 align_up( addr, 2 ) */
-      if( t + 14u > re ) break;                    /* every field read lies inside the frag (fd_txn_parse output does) */
-      uint8_t const * txn = a.span + t;
-      if( span_ld16( txn + 12 ) >= psz ) break;                                   /* :112-115 */
-      uint64_t c = txn[1];
-      uint64_t s_ = ro + span_ld16( txn + 2 ), p_ = ro + span_ld16( txn + 10 ), m_ = span_ld16( txn + 4 );
-      if( s_ + 8u > re ) break;
-      uint8_t const * sg = a.span + s_;
-#pragma unroll
-      for( int b=7; b>=0; b-- ) tag = (tag << 8) | sg[b];
-      if( m_ > psz || psz > sz ) break;
-      if( !c || c > 16u ) { st = FD_TXN_VERIFY_FAILED; break; }                  /* batch_sz 0 or > 16 -> ERR_SIG */
-      if( c * FD_FRAG_SIG_BYTES > sz ) break;                                     /* more signatures than the frag holds */
-      if( s_ + 64u*c > re || p_ + 32u*c > re ) break;
-      st = 0; cnt = (uint32_t)c; so = (uint32_t)s_; po = (uint32_t)p_; mo = (uint32_t)(ro + m_); ms = (uint32_t)(psz - m_);
-    } while( 0 );
+    frag_fields r = frag_parse_one( a, i );
     uint32_t btot;
-    uint32_t excl = frag_block_scan( cnt, wsum, &btot );                        /* (its first barrier frees s_base) */
+    uint32_t excl = frag_block_scan( r.cnt, wsum, &btot );                      /* (its first barrier frees s_base) */
     if( threadIdx.x < 64u ) {                                                   /* wave 0: the look-back */
       int late = 0;
       uint32_t base = frag_lookback( a.flag, tl, btot, a.epoch, &late );
@@ -2043,19 +2101,92 @@ fd_frag_parse_kernel( fparse_args a ) {
       }
     }
     __syncthreads();
-    uint32_t first = s_base + excl;
-    if( i < a.n ) {
-      a.status[ i ] = (int8_t)st; a.tag[ i ] = tag; a.first[ i ] = first;
-      a.fold[ i ] = cnt;
-      if( st ) ((uint4 *)a.hrec)[ i ] = make_uint4( (uint32_t)tag, (uint32_t)(tag >> 32), (uint32_t)(int32_t)st, 0u );   /* no descriptors: final */
-      for( uint32_t j=0; j<cnt && (uint64_t)first + j < a.desc_cap; j++ ) {
-        fd_ed25519_desc_t d;
-        d.sig_off = so + 64u*j; d.pub_off = po + 32u*j; d.msg_off = mo;
-        d.msg_sz = (uint16_t)ms; d.txn_idx = (uint16_t)i;
-        a.desc[ first + j ] = d;
-      }
-    }
+    frag_write<false>( a, i, r, s_base + excl );
   }
+}
+
+/* The pipelined kernel's in-launch parse (frag batches, pipe_args.aparse):
+   the four phase-A waves of the launch's first gp workgroups parse the
+   batch's tiles (workgroup g: tiles g, g + gp, ...; gp <= the CUs, and
+   these workgroups are dispatched first, so they are co-resident and their
+   look-back waits end), as fd_frag_parse_kernel does, but they cannot use a
+   workgroup barrier (the phase-B / C waves of the workgroup never reach
+   one): the four waves meet on an LDS counter instead.  A tile's look-back
+   word goes to FD_LB_DONE once all of its descriptors are stored.  Then
+   every workgroup's wave 0 waits until the tiles holding its descriptors
+   [b0, b0 + 256) are DONE and returns the count its phase A may use (the
+   batch's total if that ends inside the workgroup's range, else b0 + 256).
+   Waits are bounded; an expired wait fails the batch (fparse_args.err). */
+#define FD_LB_DONE 3ull
+__device__ __forceinline__ void wave4_meet( uint32_t * ctr, uint32_t gen, int lane, int * late ) {
+  __builtin_amdgcn_fence( __ATOMIC_RELEASE, "workgroup" );
+  if( lane == 0 ) __hip_atomic_fetch_add( ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP );
+  uint32_t i;
+  for( i=0; i<FD_LB_SPIN && __hip_atomic_load( ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP ) < 4u*gen; i++ )
+    __builtin_amdgcn_s_sleep( 1 );
+  if( i == FD_LB_SPIN ) *late = 1;
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "workgroup" );
+}
+
+__device__ __forceinline__ uint32_t pipe_aparse( fparse_args const & a, uint64_t gp, uint32_t * s_ap, int wv, int lane ) {
+  int late = 0;
+  uint32_t gen = 0u;
+  uint64_t ntile = (a.n + FD_FRAG_BLOCK - 1u) / FD_FRAG_BLOCK;
+  uint64_t ep = (uint64_t)a.epoch << 32;
+  for( uint64_t tl=blockIdx.x; blockIdx.x<gp && tl<ntile; tl+=gp ) {
+    uint64_t i = tl * FD_FRAG_BLOCK + (uint64_t)(wv*64 + lane);
+    frag_fields r = frag_parse_one( a, i );
+    uint32_t v = r.cnt;
+#pragma unroll
+    for( uint32_t o=1u; o<64u; o<<=1 ) { uint32_t y = __shfl_up( v, o, 64 ); if( lane >= (int)o ) v += y; }
+    if( lane == 63 ) s_ap[ wv ] = v;
+    wave4_meet( s_ap + 6, ++gen, lane, &late );                 /* the four wave totals */
+    uint32_t pre = 0u, all = 0u;
+#pragma unroll
+    for( int k=0; k<4; k++ ) { uint32_t t = s_ap[ k ]; pre += k < wv ? t : 0u; all += t; }
+    if( wv == 0 ) {
+      uint32_t base = frag_lookback( a.flag, tl, all, a.epoch, &late );
+      if( lane == 0 ) { s_ap[ 4 ] = base; if( tl == ntile - 1u ) *a.total = base + all; }
+    }
+    wave4_meet( s_ap + 6, ++gen, lane, &late );                 /* the tile's base */
+    uint32_t base = s_ap[ 4 ];
+    frag_write<true>( a, i, r, base + pre + v - r.cnt );
+    __builtin_amdgcn_s_waitcnt( 0x0F70 );                       /* vmcnt(0): this wave's stores are done */
+    wave4_meet( s_ap + 6, ++gen, lane, &late );                 /* all four waves' stores */
+    if( wv == 0 && lane == 0 )
+      __hip_atomic_store( a.flag + tl, ep | (FD_LB_DONE << 30) | ((base + all) & 0x3fffffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  }
+  /* wave 0: wait for the tiles that hold descriptors [b0, b0 + 256) */
+  if( wv == 0 ) {
+    uint64_t need = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK + FD_VERIFY_BLOCK;
+    uint32_t nn = 0u, spin = 0u;
+    int64_t top = 0;
+    while( ntile ) {
+      int64_t k = top + lane;
+      uint64_t w = k < (int64_t)ntile ? __hip_atomic_load( a.flag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) : 0ull;
+      bool done = (w & 0xffffffff00000000ull) == ep && ((w >> 30) & 3ull) == FD_LB_DONE;
+      uint32_t P = (uint32_t)(w & 0x3fffffffull);
+      uint64_t term = __ballot( done && (k == (int64_t)ntile - 1 || (uint64_t)P >= need) );
+      uint64_t nd = __ballot( k < (int64_t)ntile && !done );
+      uint64_t before = term ? (term & (~term + 1ull)) - 1ull : ~0ull;   /* lanes before the first terminal one */
+      if( nd & before ) {
+        if( ++spin > FD_LB_SPIN ) { late = 1; break; }
+        __builtin_amdgcn_s_sleep( 1 );
+        continue;
+      }
+      if( term ) {
+        int f = __builtin_ctzll( term );
+        uint32_t Pf = __shfl( P, f, 64 );
+        nn = (uint64_t)Pf >= need ? (uint32_t)need : Pf;
+        break;
+      }
+      top += 64;
+    }
+    if( lane == 0 ) s_ap[ 5 ] = nn;
+  }
+  wave4_meet( s_ap + 6, ++gen, lane, &late );
+  if( late && lane == 0 && a.err ) __hip_atomic_store( a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+  return s_ap[ 5 ];
 }
 
 /* Each frag's verify code from its descriptors' codes, with

@@ -55,10 +55,13 @@ def load_lib():
     if _LIB is not None:
         return _LIB
     path = lib_path()
-    try:  # share torch's HIP runtime if torch is used in this process (same SONAME, one runtime)
-        import torch  # noqa: F401
-    except Exception:
-        pass
+    # share torch's HIP runtime if torch is used in this process (same SONAME, one runtime);
+    # FD_ED25519_GPU_NO_TORCH=1: the HIP runtime the library links (/opt/rocm), torch not loaded
+    if os.environ.get("FD_ED25519_GPU_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
     if not os.path.exists(path):
         raise GpuError("libfd_ed25519_gpu.so not built (run `make -C firedancer_amd` or __graft_entry__.build())")
     lib = ctypes.CDLL(path)

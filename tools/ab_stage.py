@@ -7,7 +7,7 @@ created under its environment (read at context creation).  Prints the median
 streaming rate per setting and checks every setting's results equal the
 first's.
 
-  python3 tools/ab_stage.py "A:" "B:FD_ED25519_GPU_PARSE_STREAM=0" [--frags N] [--rounds R]
+  python3 tools/ab_stage.py "A:" "B:FD_ED25519_GPU_PARSE_STREAM=1" [--frags N] [--rounds R]
 """
 import argparse
 import os
