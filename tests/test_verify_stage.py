@@ -685,29 +685,32 @@ def test_stage_in_launch_parse_vs_parse_launch(monkeypatch):
     """The pipelined path's in-launch parse (the verify launch's phase-A waves
     parse the batch's frags, look-back scan and all, then wait for the tiles
     holding their descriptors) against a parse launch first
-    (FD_ED25519_GPU_APARSE=0), frag for frag, over four batches of one stream:
-    33,000 frags of 1-8 signatures with a third of them made BAD_FRAG in runs
-    (so descriptors are sparse and a workgroup's descriptors come from tiles
-    far from its own index), a batch with no valid frag (count 0) and a
-    batch of one frag."""
+    (FD_ED25519_GPU_APARSE=0), frag for frag, over one stream of five
+    batches: 33,000 frags of 1-8 signatures with a third of them made
+    BAD_FRAG in runs (so descriptors are sparse and a workgroup's descriptors
+    come from tiles far from its own index), a 66,000-frag batch (above one
+    wave per SIMD: a parse launch and the one-shot kernels, between pipelined
+    batches), a batch with no valid frag (count 0), a batch of one frag and
+    the first batch reversed."""
     rng = np.random.default_rng(4242)
     arena_u, frags_u = _random_frag_stream(rng, 2500, 2500)
-    n = 33000
-    order = rng.integers(0, len(frags_u), size=n)
-    frags = np.zeros(n, frags_u.dtype)
-    frags["off"] = frags_u["off"][order]
-    frags["sz"] = frags_u["sz"][order]
+    n, n_big = 33000, 66000
+    order = rng.integers(0, len(frags_u), size=n_big)
+    big = np.zeros(n_big, frags_u.dtype)
+    big["off"] = frags_u["off"][order]
+    big["sz"] = frags_u["sz"][order]
+    frags = big[:n].copy()
     for s0 in range(0, n, 3000):                       # runs of frags past the arena: BAD_FRAG
         frags["off"][s0:s0 + int(rng.integers(200, 1500))] = len(arena_u) + 64
     allbad = frags[:700].copy()
     allbad["off"] = len(arena_u) + 64
-    batches = [frags, allbad, frags[5:6], frags[::-1].copy()]
+    batches = [frags, big, allbad, frags[5:6].copy(), frags[::-1].copy()]
     out = {}
     for ap in ("1", "0"):
         monkeypatch.setenv("FD_ED25519_GPU_APARSE", ap)
-        g = fa.Ed25519Gpu(device_mask=1, max_batch=16 * n)
+        g = fa.Ed25519Gpu(device_mask=1, max_batch=16 * n_big)
         try:
-            ast = fa.AsyncStage(g, fa.TCache(), n, threads=8, device_parse=True)
+            ast = fa.AsyncStage(g, fa.TCache(), n_big, threads=8, device_parse=True)
             res = [np.zeros(len(b), np.int8) for b in batches]
             sig = [np.zeros(len(b), np.uint64) for b in batches]
             for b, r, s in zip(batches, res, sig):
@@ -715,7 +718,8 @@ def test_stage_in_launch_parse_vs_parse_launch(monkeypatch):
             while ast.pending():
                 ast.poll(True)
             ast.close()
-            assert g.launch_stats()[0] > 0                 # the pipelined kernel ran
+            pipe_l, one_l = g.launch_stats()
+            assert pipe_l > 0 and one_l > 0, (pipe_l, one_l)  # both kernels ran
         finally:
             g.close()
         out[ap] = (res, sig)
@@ -724,4 +728,4 @@ def test_stage_in_launch_parse_vs_parse_launch(monkeypatch):
         assert len(bad) == 0, (k, [(int(j), int(out["1"][0][k][j]), int(out["0"][0][k][j])) for j in bad[:10]])
     hist = {int(c): int(v) for c, v in zip(*np.unique(out["1"][0][0], return_counts=True))}
     assert hist.get(S, 0) > 1000 and hist.get(BAD, 0) > 3000, hist
-    assert np.all(out["1"][0][1] == BAD)
+    assert np.all(out["1"][0][2] == BAD)
