@@ -55,6 +55,12 @@
 #ifndef FD_OPT_TAIL1
 #define FD_OPT_TAIL1 1
 #endif
+/*   APARSE    (round 5) the pipelined kernel's phase A can parse its frag
+               batch in the launch (pipe_aparse); 0 compiles that path out
+               (an A/B of what its code costs the launches that do not use it). */
+#ifndef FD_OPT_APARSE
+#define FD_OPT_APARSE 1
+#endif
 
 /* Diagnostic build only (-DFD_PHASE_STAMPS, tools/Makefile): s_memtime at
    phase boundaries, per-wave deltas summed into args.stamps.  The product
@@ -1298,9 +1304,12 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
   if( role == 2 ) {
     /* ---- phase A, batch j ---- */
     uint64_t nn = args.n;                                               /* args.cnt: a device-side count <= n */
+#if FD_OPT_APARSE
     if( a.aparse )                   /* the batch's frags parsed in this launch: the count this workgroup may use */
       nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)pipe_aparse( a.fp, a.aparse, s_ap, wv, lane ) ) );
-    else if( args.cnt ) nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)*args.cnt ) );
+    else
+#endif
+    if( args.cnt ) nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)*args.cnt ) );
     uint64_t b0 = (uint64_t)blockIdx.x * FD_VERIFY_BLOCK, di = gid;   /* di: the descriptor this lane verifies */
     if( a.lsort && b0 + FD_VERIFY_BLOCK <= nn )                       /* full workgroups only: all four waves here */
       di = b0 + pipe_len_order( len_bucket( a.aparse ? desc_ld_coh( args.desc + gid ) : args.desc[ gid ] ), wv, lane, s_lo, s_lo + 4*FD_LEN_NB,
