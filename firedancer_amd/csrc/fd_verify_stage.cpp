@@ -372,6 +372,7 @@ extern "C" int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t * ctx, uint8_t cons
                                             fd_ed25519_gpu_frag_t const * frag, uint64_t n, int8_t * status,
                                             uint64_t * tag );
 extern "C" int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t * ctx, int block );
+extern "C" int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t * ctx );
 extern "C" int fd_ed25519_gpu_poll_block( fd_ed25519_gpu_t * ctx );
 extern "C" uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx );
 extern "C" int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n );
@@ -420,6 +421,7 @@ struct fd_ed25519_gpu_stage {
   int                       threads;
   int                       devparse;      /* parse frags on the GPU when the context has room */
   int                       autoreg;       /* page-lock callers' frag areas (opt-in: FD_ED25519_GPU_STAGE_AUTOREG=1) */
+  int                       kick;          /* early drain launches when nothing waits (FD_ED25519_GPU_STAGE_KICK=0: off, A/B) */
   int                       head;          /* oldest pending slot */
   int                       pending;       /* 0..FD_VS_DEPTH */
   vs_batch                  b[ FD_VS_DEPTH ];
@@ -660,6 +662,18 @@ vs_poller( fd_ed25519_gpu_stage_t * st ) {
     uint64_t t0 = vs_now();
     int r = b->devp ? fd_ed25519_gpu_frags_poll( st->ctx, 0 ) : fd_ed25519_gpu_poll( st->ctx );
     st->stats.gpu_poll_ns += vs_now() - t0;
+    if( r == FD_ED25519_GPU_PENDING && b->devp && st->kick ) {
+      /* nothing waits to be launched: the pipe's last batches get their
+         drain launches now (behind the running launch) instead of once the
+         GPU has gone idle and a poll has seen it -- ~150 us of idle GPU
+         before each of the two drains in the traces (profiles/r05/stage) */
+      bool waiting = false;
+      for( int j=0; j<st->pending && !waiting; j++ ) waiting = st->b[ (st->head + j) % FD_VS_DEPTH ].state == 1;
+      if( !waiting ) {
+        int kr = fd_ed25519_gpu_frags_kick( st->ctx );
+        if( kr ) r = kr;
+      }
+    }
     if( r == FD_ED25519_GPU_PENDING ) {
       /* the GPU is still at it: back off without the lock.  A batch is
          ~0.6 ms of GPU work, so the poller spins (yielding) through a
@@ -740,6 +754,7 @@ fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, 
   st->ctx = ctx; st->tc = tc; st->max_frags = max_frags;
   st->threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
   st->devparse = 1;
+  { char const * k = getenv( "FD_ED25519_GPU_STAGE_KICK" ); st->kick = !(k && k[0] == '0'); }
   char const * e = getenv( "FD_ED25519_GPU_STAGE_AUTOREG" );        /* "1": page-lock callers' frag areas */
   st->autoreg = e && e[0] == '1';
   memset( &st->stats, 0, sizeof(st->stats) );
