@@ -109,7 +109,11 @@ struct fparse_args {
   uint64_t *                     tag;        /* out */
   uint32_t *                     first;      /* out: the frag's first descriptor index */
   uint64_t *                     fold;       /* out: the fold word (FD_FOLD_SH), set to the descriptor count */
-  uint64_t *                     flag;       /* look-back words, one per workgroup (zeroed once at allocation) */
+  uint64_t *                     flag;       /* look-back words, one per tile (zeroed once at allocation) */
+  uint64_t *                     tctr;       /* the in-launch parse's tile counter (zeroed once, never reset) */
+  uint64_t                       tbase;      /* its value when this batch's launch starts: every workgroup takes
+                                                tiles until one is past the batch, so a launch of G workgroups over
+                                                T tiles adds T + G (the host keeps the sum) */
   uint32_t *                     total;      /* out: descriptor count */
   uint32_t *                     err;        /* host-mapped: 1 if a look-back wait expired (the batch fails) */
   fd_ed25519_desc_t *            desc;       /* out: descriptors */

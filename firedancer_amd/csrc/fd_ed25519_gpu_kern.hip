@@ -1257,7 +1257,7 @@ __device__ __forceinline__ void hand_to_lds( uint32_t * y, uint32_t const * hand
   for( int j=0; j<24; j++ ) if( j < nwords ) y[ j*64 + lane ] = t[j];
 }
 
-__device__ __forceinline__ uint32_t pipe_aparse( fparse_args const & a, uint64_t gp, uint32_t * s_ap, int wv, int lane );
+__device__ __forceinline__ uint32_t pipe_aparse( fparse_args const & a, uint32_t * s_ap, int wv, int lane );
 __device__ __forceinline__ fd_ed25519_desc_t desc_ld_coh( fd_ed25519_desc_t const * p );
 
 extern "C" __global__ void __launch_bounds__( 3 * FD_VERIFY_BLOCK, 1 )
@@ -1306,7 +1306,7 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
     uint64_t nn = args.n;                                               /* args.cnt: a device-side count <= n */
 #if FD_OPT_APARSE
     if( a.aparse )                   /* the batch's frags parsed in this launch: the count this workgroup may use */
-      nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)pipe_aparse( a.fp, a.aparse, s_ap, wv, lane ) ) );
+      nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)pipe_aparse( a.fp, s_ap, wv, lane ) ) );
     else
 #endif
     if( args.cnt ) nn = min( nn, (uint64_t)__builtin_amdgcn_readfirstlane( (int)*args.cnt ) );
@@ -2115,17 +2115,22 @@ fd_frag_parse_kernel( fparse_args a ) {
 }
 
 /* The pipelined kernel's in-launch parse (frag batches, pipe_args.aparse):
-   the four phase-A waves of the launch's first gp workgroups parse the
-   batch's tiles (workgroup g: tiles g, g + gp, ...; gp <= the CUs, and
-   these workgroups are dispatched first, so they are co-resident and their
-   look-back waits end), as fd_frag_parse_kernel does, but they cannot use a
-   workgroup barrier (the phase-B / C waves of the workgroup never reach
-   one): the four waves meet on an LDS counter instead.  A tile's look-back
-   word goes to FD_LB_DONE once all of its descriptors are stored.  Then
-   every workgroup's wave 0 waits until the tiles holding its descriptors
-   [b0, b0 + 256) are DONE and returns the count its phase A may use (the
-   batch's total if that ends inside the workgroup's range, else b0 + 256).
-   Waits are bounded; an expired wait fails the batch (fparse_args.err). */
+   the four phase-A waves of every workgroup take the batch's tiles of 256
+   frags from a counter, in order (tile IDs by one atomic add each, not by
+   workgroup index), and parse each as fd_frag_parse_kernel does: the per-frag fields,
+   the tile's scan, its base by the decoupled look-back, its descriptors.  A
+   tile's look-back only waits on tiles taken before it, by workgroups that
+   were running when they took them, so every wait ends whether or not the
+   launch's workgroups are all resident at once (another kernel on the GPU,
+   a grid above one workgroup per CU).  The four waves cannot use a
+   workgroup barrier (the workgroup's phase-B / C waves never reach one): they
+   meet on an LDS counter instead.  A tile's look-back word goes to
+   FD_LB_DONE once all of its descriptors are stored.  Once no tile is left,
+   wave 0 waits until the tiles holding the workgroup's descriptors
+   [b0, b0 + 256) are DONE -- all taken by running workgroups, so they will
+   be -- and returns the count its phase A may use (the batch's total if that
+   ends inside the workgroup's range, else b0 + 256).  Waits are bounded; an
+   expired wait fails the batch (fparse_args.err). */
 #define FD_LB_DONE 3ull
 __device__ __forceinline__ void wave4_meet( uint32_t * ctr, uint32_t gen, int lane, int * late ) {
   __builtin_amdgcn_fence( __ATOMIC_RELEASE, "workgroup" );
@@ -2137,12 +2142,18 @@ __device__ __forceinline__ void wave4_meet( uint32_t * ctr, uint32_t gen, int la
   __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "workgroup" );
 }
 
-__device__ __forceinline__ uint32_t pipe_aparse( fparse_args const & a, uint64_t gp, uint32_t * s_ap, int wv, int lane ) {
+__device__ __forceinline__ uint32_t pipe_aparse( fparse_args const & a, uint32_t * s_ap, int wv, int lane ) {
   int late = 0;
   uint32_t gen = 0u;
   uint64_t ntile = (a.n + FD_FRAG_BLOCK - 1u) / FD_FRAG_BLOCK;
   uint64_t ep = (uint64_t)a.epoch << 32;
-  for( uint64_t tl=blockIdx.x; blockIdx.x<gp && tl<ntile; tl+=gp ) {
+  for(;;) {
+    if( wv == 0 && lane == 0 )          /* one relaxed add per take: no retry loop on the shared word */
+      s_ap[ 7 ] = (uint32_t)min( __hip_atomic_fetch_add( a.tctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) - a.tbase,
+                                 (uint64_t)ntile );
+    wave4_meet( s_ap + 6, ++gen, lane, &late );                 /* the tile this workgroup takes */
+    uint64_t tl = s_ap[ 7 ];
+    if( tl >= ntile ) break;
     uint64_t i = tl * FD_FRAG_BLOCK + (uint64_t)(wv*64 + lane);
     frag_fields r = frag_parse_one( a, i );
     uint32_t v = r.cnt;

@@ -729,3 +729,64 @@ def test_stage_in_launch_parse_vs_parse_launch(monkeypatch):
     hist = {int(c): int(v) for c, v in zip(*np.unique(out["1"][0][0], return_counts=True))}
     assert hist.get(S, 0) > 1000 and hist.get(BAD, 0) > 3000, hist
     assert np.all(out["1"][0][2] == BAD)
+
+
+@pytest.mark.gpu
+def test_stage_in_launch_parse_two_contexts_concurrently():
+    """Two contexts on one GPU, each with its own stage, fed from two threads
+    at once: their pipelined verify launches share the CUs, so a launch's
+    workgroups are not all resident together.  The in-launch parse takes its
+    tiles from a counter in order, so its waits still end; both streams
+    (frags with runs of BAD_FRAG, so descriptors are sparse across tiles)
+    give the results of one context alone."""
+    import threading
+    rng = np.random.default_rng(99)
+    arena_u, frags_u = _random_frag_stream(rng, 2500, 2500)
+    n = 30000
+    streams = []
+    for k in range(2):
+        order = rng.integers(0, len(frags_u), size=n)
+        fr = np.zeros(n, frags_u.dtype)
+        fr["off"] = frags_u["off"][order]
+        fr["sz"] = frags_u["sz"][order]
+        for s0 in range(0, n, 2500):
+            fr["off"][s0:s0 + int(rng.integers(300, 1800))] = len(arena_u) + 64
+        streams.append([fr[j:j + 10000].copy() for j in range(0, n, 10000)] * 3)
+
+    def run(g, batches, res, sig, errs):
+        try:
+            ast = fa.AsyncStage(g, fa.TCache(), 10000, threads=4, device_parse=True)
+            for b, r, s in zip(batches, res, sig):
+                ast.submit(arena_u, len(arena_u), np.ascontiguousarray(b), r, s)
+            while ast.pending():
+                ast.poll(True)
+            ast.close()
+        except Exception as e:                          # noqa: BLE001
+            errs.append(e)
+
+    ctxs = [fa.Ed25519Gpu(device_mask=1, max_batch=16 * 10000) for _ in range(2)]
+    try:
+        out = {}
+        for mode in ("alone", "together"):
+            res = [[np.zeros(len(b), np.int8) for b in streams[k]] for k in range(2)]
+            sig = [[np.zeros(len(b), np.uint64) for b in streams[k]] for k in range(2)]
+            errs = []
+            if mode == "alone":
+                for k in range(2):
+                    run(ctxs[k], streams[k], res[k], sig[k], errs)
+            else:
+                th = [threading.Thread(target=run, args=(ctxs[k], streams[k], res[k], sig[k], errs)) for k in range(2)]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join(120)
+                assert not any(t.is_alive() for t in th), "a stage did not finish"
+            assert not errs, errs
+            out[mode] = (res, sig)
+        for k in range(2):
+            for j in range(len(streams[k])):
+                assert np.array_equal(out["alone"][0][k][j], out["together"][0][k][j]), (k, j)
+                assert np.array_equal(out["alone"][1][k][j], out["together"][1][k][j]), (k, j)
+    finally:
+        for g in ctxs:
+            g.close()
