@@ -57,7 +57,8 @@
 #endif
 /*   APARSE    (round 5) the pipelined kernel's phase A can parse its frag
                batch in the launch (pipe_aparse); 0 compiles that path out
-               (an A/B of what its code costs the launches that do not use it). */
+               (an A/B of what its code costs the launches that do not use it;
+               such a build runs frag batches only with FD_ED25519_GPU_APARSE=0). */
 #ifndef FD_OPT_APARSE
 #define FD_OPT_APARSE 1
 #endif
