@@ -372,7 +372,7 @@ extern "C" int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t * ctx, uint8_t cons
                                             fd_ed25519_gpu_frag_t const * frag, uint64_t n, int8_t * status,
                                             uint64_t * tag );
 extern "C" int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t * ctx, int block );
-extern "C" int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t * ctx );
+extern "C" int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t * ctx, int oldest );
 extern "C" int fd_ed25519_gpu_poll_block( fd_ed25519_gpu_t * ctx );
 extern "C" uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx );
 extern "C" int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n );
@@ -421,7 +421,8 @@ struct fd_ed25519_gpu_stage {
   int                       threads;
   int                       devparse;      /* parse frags on the GPU when the context has room */
   int                       autoreg;       /* page-lock callers' frag areas (opt-in: FD_ED25519_GPU_STAGE_AUTOREG=1) */
-  int                       kick;          /* early drain launches when nothing waits (FD_ED25519_GPU_STAGE_KICK=0: off, A/B) */
+  int                       kick;          /* early drain launches when nothing waits: 1 the oldest batch's (default),
+                                              2 the newest's, 0 none (FD_ED25519_GPU_STAGE_KICK, A/Bs) */
   int                       head;          /* oldest pending slot */
   int                       pending;       /* 0..FD_VS_DEPTH */
   vs_batch                  b[ FD_VS_DEPTH ];
@@ -670,7 +671,7 @@ vs_poller( fd_ed25519_gpu_stage_t * st ) {
       bool waiting = false;
       for( int j=0; j<st->pending && !waiting; j++ ) waiting = st->b[ (st->head + j) % FD_VS_DEPTH ].state == 1;
       if( !waiting ) {
-        int kr = fd_ed25519_gpu_frags_kick( st->ctx );
+        int kr = fd_ed25519_gpu_frags_kick( st->ctx, st->kick == 1 );
         if( kr ) r = kr;
       }
     }
@@ -754,7 +755,8 @@ fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, 
   st->ctx = ctx; st->tc = tc; st->max_frags = max_frags;
   st->threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
   st->devparse = 1;
-  { char const * k = getenv( "FD_ED25519_GPU_STAGE_KICK" ); st->kick = !(k && k[0] == '0'); }
+  { char const * k = getenv( "FD_ED25519_GPU_STAGE_KICK" );         /* "0" off, "2" the newest batch's drains (A/Bs) */
+    st->kick = k && k[0] == '0' ? 0 : k && k[0] == '2' ? 2 : 1; }
   char const * e = getenv( "FD_ED25519_GPU_STAGE_AUTOREG" );        /* "1": page-lock callers' frag areas */
   st->autoreg = e && e[0] == '1';
   memset( &st->stats, 0, sizeof(st->stats) );

@@ -73,7 +73,7 @@ int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n ) { (void)c
 int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t *, uint8_t const *, uint64_t, fd_ed25519_gpu_frag_t const *, uint64_t,
                                  int8_t *, uint64_t * ) { return FD_ED25519_GPU_ERR_ARG; }
 int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t *, int ) { return FD_ED25519_GPU_OK; }
-int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t * ) { return FD_ED25519_GPU_OK; }
+int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t *, int ) { return FD_ED25519_GPU_OK; }
 int fd_ed25519_gpu_host_register_auto( fd_ed25519_gpu_t *, void *, uint64_t ) { return 1; }   /* "the caller's" */
 int fd_ed25519_gpu_host_unregister( fd_ed25519_gpu_t *, void * ) { return FD_ED25519_GPU_OK; }
 /* the shred path's GPU half: reads every byte the root kernel would (leaf,
