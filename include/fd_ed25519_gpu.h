@@ -408,14 +408,17 @@ typedef struct {
 } fd_ed25519_gpu_stage_stats_t;
 int  fd_ed25519_gpu_stage_stats      ( fd_ed25519_gpu_stage_t * st, fd_ed25519_gpu_stage_stats_t * out );
 int  fd_ed25519_gpu_stage_stats_reset( fd_ed25519_gpu_stage_t * st );
-/* By default the stage parses frags on the GPU (the frags' arena span is
-   copied to HBM; parse, descriptor emission, verify and the per-frag fold
-   run there; the host only replays the tcache), falling back to the host
-   parse when the context's max_batch is below 16 x frags per device.  One
-   difference from the host parse: a frag whose fd_txn_t places signatures /
-   pubkeys / message outside the batch's frag span (impossible for
-   fd_txn_parse output) is BAD_FRAG on the GPU.  on = 0 selects the host
-   parse (no batches may be pending). */
+/* By default the stage parses frags on the GPU (the page runs the frags
+   occupy are copied to HBM; parse, descriptors, verify and the per-frag
+   fold run there -- for batches of at most one wave per SIMD in ONE launch
+   per batch, the pipelined verify launch parsing its own frags and its
+   phase C folding each frag's codes into page-locked staging; the host
+   only replays the tcache), falling back to the host parse when the
+   context's max_batch is below 16 x frags per device.  One difference from
+   the host parse: a frag whose fd_txn_t places its header, signatures,
+   pubkeys or message outside the frag's own bytes (impossible for
+   fd_txn_parse output) is BAD_FRAG -- in both parses.  on = 0 selects the
+   host parse (no batches may be pending). */
 int  fd_ed25519_gpu_stage_set_device_parse( fd_ed25519_gpu_stage_t * st, int on );
 
 /* Runs throw-away full-size batches (one short frag at the start of arena,
