@@ -790,3 +790,34 @@ def test_stage_in_launch_parse_two_contexts_concurrently():
     finally:
         for g in ctxs:
             g.close()
+
+
+@pytest.mark.gpu
+def test_stage_in_launch_parse_small_signature_bound(monkeypatch):
+    """A pipelined frag batch whose host-side signature bound is tiny (30,000
+    64-byte junk frags bound no signature) but whose parse has 118 tiles:
+    the launch still gets a workgroup per tile to parse them, and the valid
+    frags behind the junk verify -- against a parse launch first
+    (FD_ED25519_GPU_APARSE=0), frag for frag."""
+    rng = np.random.default_rng(7)
+    arena_u, frags_u = _random_frag_stream(rng, 200, 200)
+    junk = np.zeros(30000, frags_u.dtype)
+    junk["off"] = rng.integers(0, len(arena_u) - 64, size=len(junk)).astype(np.uint32)
+    junk["sz"] = 64
+    batch = np.concatenate([junk, frags_u[:150]])
+    out = {}
+    for ap in ("1", "0"):
+        monkeypatch.setenv("FD_ED25519_GPU_APARSE", ap)
+        g = fa.Ed25519Gpu(device_mask=1, max_batch=16 * len(batch))
+        try:
+            ast = fa.AsyncStage(g, fa.TCache(), len(batch), threads=4, device_parse=True)
+            res = np.zeros(len(batch), np.int8); sig = np.zeros(len(batch), np.uint64)
+            ast.submit(arena_u, len(arena_u), np.ascontiguousarray(batch), res, sig)
+            while ast.pending():
+                ast.poll(True)
+            ast.close()
+        finally:
+            g.close()
+        out[ap] = (res, sig)
+    assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
+    assert np.count_nonzero(out["1"][0][len(junk):] == S) > 50
