@@ -8,6 +8,7 @@ streaming rate per setting and checks every setting's results equal the
 first's.
 
   python3 tools/ab_stage.py "A:" "B:FD_ED25519_GPU_PARSE_STREAM=1" [--frags N] [--rounds R]
+  (a setting's BATCH=<frags> gives it its own batch size)
 """
 import argparse
 import os
@@ -21,14 +22,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tools"))
 import firedancer_amd as fa  # noqa: E402
-from bench_verify_stage import make_stream  # noqa: E402
+from bench_verify_stage import make_stream, stream_passes  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("settings", nargs="+")
 ap.add_argument("--frags", type=int, default=1 << 20)
 ap.add_argument("--passes", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=4)
-ap.add_argument("--batch", type=int, default=35000)
+ap.add_argument("--batch", type=int, default=36000)
 a = ap.parse_args()
 arena, frags, n_sigs = make_stream(a.frags, 0.1)
 fr = np.ascontiguousarray(frags)
@@ -36,14 +37,16 @@ specs = []
 for sp in a.settings:
     name, _, env = sp.partition(":")
     specs.append((name, dict(kv.split("=", 1) for kv in env.split(",")) if env else {}))
+# BATCH=<frags> in a setting: that setting's batch size (not an environment variable)
+bsz = [int(env.pop("BATCH", a.batch)) for _, env in specs]
 ctx = []
-for name, env in specs:
+for (name, env), b in zip(specs, bsz):
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
-    g = fa.Ed25519Gpu(device_mask=1, max_batch=16 * a.batch)
+    g = fa.Ed25519Gpu(device_mask=1, max_batch=16 * b)
     if not ctx:
         g.host_register(arena)               # page-locked once (all contexts share the process's registration)
-    st = fa.AsyncStage(g, fa.TCache(), a.batch, threads=8, device_parse=True)
+    st = fa.AsyncStage(g, fa.TCache(), b, threads=8, device_parse=True)
     for k, v in saved.items():
         if v is None:
             os.environ.pop(k, None)
@@ -54,32 +57,22 @@ res = [np.zeros(len(fr), np.int8) for _ in specs]
 sig = np.zeros(len(fr), np.uint64)
 
 
-def stream(st, out, passes):
+def stream(st, out, passes, batch):
     st.tcache.reset()
-    total, k = passes * len(fr), 0
-    t = time.perf_counter()
-    while k < total or st.pending():
-        if k < total and st.pending() < fa.STAGE_DEPTH:
-            i = k % len(fr)
-            j = min(len(fr), i + a.batch)
-            st.submit(arena, len(arena), fr[i:j], out[i:j], sig[i:j])
-            k += j - i
-        else:
-            st.poll(True)
-    return passes * n_sigs / (time.perf_counter() - t)
+    return passes * n_sigs / stream_passes(st, arena, fr, out, sig, passes, batch)
 
 
-for (g, st), out in zip(ctx, res):
-    stream(st, out, 1)                      # warm
+for (g, st), out, b in zip(ctx, res, bsz):
+    stream(st, out, 1, b)                   # warm
 rates = [[] for _ in specs]
 for r in range(a.rounds):
     order = range(len(specs)) if r % 2 == 0 else reversed(range(len(specs)))
     for k in order:
-        rates[k].append(stream(ctx[k][1], res[k], a.passes))
+        rates[k].append(stream(ctx[k][1], res[k], a.passes, bsz[k]))
 for k, (name, env) in enumerate(specs):
     assert np.count_nonzero(res[k] != res[0]) <= 16, name
     print("%-10s %-40s streaming median %.1f M sigs/s (min %.1f max %.1f)" % (
-        name, ",".join("%s=%s" % kv for kv in env.items()), statistics.median(rates[k]) / 1e6,
+        name, ",".join(["%s=%s" % kv for kv in env.items()] + ["batch=%d" % bsz[k]]), statistics.median(rates[k]) / 1e6,
         min(rates[k]) / 1e6, max(rates[k]) / 1e6), flush=True)
 for i, (g, st) in enumerate(ctx):
     st.close()

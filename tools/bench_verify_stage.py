@@ -42,6 +42,42 @@ def make_stream(n_frags, dup, seed=5):
     return arena, frags, sum(cnts[i] for i in order)
 
 
+def stream_passes(ast, arena, fr, res, sig, passes, batch):
+    """`passes` passes over the frags fr as ONE stream into the async stage
+    ast, like a tile that never stops: batches of `batch` frags cut
+    continuously, so a batch may run from the end of one pass into the start
+    of the next (a tile's batch boundaries fall anywhere in its stream; cut
+    per pass, every pass would end in a remainder batch).  A batch that wraps
+    goes in as its own copy of the frag records, and its results are put back
+    in place when its poll returns.  Returns the seconds the stream took."""
+    import firedancer_amd as fa
+    n = len(fr)
+    total, k = passes * n, 0
+    fifo = []
+    t = time.perf_counter()
+    while k < total or ast.pending():
+        if k < total and ast.pending() < fa.STAGE_DEPTH:
+            i, m = k % n, min(batch, total - k)
+            if i + m <= n:
+                ast.submit(arena, len(arena), fr[i:i + m], res[i:i + m], sig[i:i + m])
+                fifo.append(None)
+            else:
+                n1 = n - i
+                fb = np.ascontiguousarray(np.concatenate([fr[i:], fr[:m - n1]]))
+                tr, ts = np.zeros(m, np.int8), np.zeros(m, np.uint64)
+                ast.submit(arena, len(arena), fb, tr, ts)
+                fifo.append((fb, tr, ts, i, n1))
+            k += m
+        else:
+            ast.poll(True)
+            w = fifo.pop(0)
+            if w:
+                fb, tr, ts, i, n1 = w
+                res[i:], sig[i:] = tr[:n1], ts[:n1]
+                res[:len(tr) - n1], sig[:len(tr) - n1] = tr[n1:], ts[n1:]
+    return time.perf_counter() - t
+
+
 def cpu_baseline(arena, frags, budget_s=10.0):
     path = os.path.join(REPO, "oracle", "_ref", "libfdref_avx512.so")
     if not os.path.exists(path):
@@ -70,7 +106,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--async-batch", type=int, default=35000)
+    # 36,000 frags: 64.0K signatures at this stream's 1.78 per frag (+-195, 7.9 sigma under the
+    # 65,536 one launch verifies in one wave per SIMD); profiles/r05/stage/ab_batch_size_stream.log
+    ap.add_argument("--async-batch", type=int, default=36000)
     args = ap.parse_args()
     import firedancer_amd as fa
 
@@ -132,18 +170,11 @@ def main():
 
             def run_stream(reps):
                 """reps passes over the frags as ONE stream (no drain between
-                passes, like a tile that never stops): the 16-deep tcache has
-                forgotten a pass's frags long before they come again"""
+                passes, like a tile that never stops; batches cut across pass
+                boundaries): the 16-deep tcache has forgotten a pass's frags
+                long before they come again"""
                 ast.tcache.reset()
-                total, k = reps * len(fr), 0
-                while k < total or ast.pending():
-                    if k < total and ast.pending() < fa.STAGE_DEPTH:
-                        i = k % len(fr)
-                        j = min(len(fr), i + ab)
-                        ast.submit(arena, len(arena), fr[i:j], res_a[i:j], sig_a[i:j])
-                        k += j - i
-                    else:
-                        ast.poll(True)
+                stream_passes(ast, arena, fr, res_a, sig_a, reps, ab)
 
             run_async()                       # first use: registration, buffers
             ast.stats(reset=True); big.host_stats(reset=True)

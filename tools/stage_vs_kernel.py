@@ -24,14 +24,14 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import torch  # noqa: E402
 import firedancer_amd as fa  # noqa: E402
 from bench import build_workload  # noqa: E402
-from bench_verify_stage import make_stream  # noqa: E402
+from bench_verify_stage import make_stream, stream_passes  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--frags", type=int, default=1 << 20)
 ap.add_argument("--passes", type=int, default=3)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--launches", type=int, default=400)
-ap.add_argument("--batch", type=int, default=35000)
+ap.add_argument("--batch", type=int, default=36000)
 a = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -68,17 +68,7 @@ sig = np.zeros(len(fr), np.uint64)
 
 def stage_rate(passes):
     st.tcache.reset()
-    total, k = passes * len(fr), 0
-    t = time.perf_counter()
-    while k < total or st.pending():
-        if k < total and st.pending() < fa.STAGE_DEPTH:
-            i = k % len(fr)
-            j = min(len(fr), i + a.batch)
-            st.submit(sarena, len(sarena), fr[i:j], res[i:j], sig[i:j])
-            k += j - i
-        else:
-            st.poll(True)
-    return passes * n_sigs / (time.perf_counter() - t)
+    return passes * n_sigs / stream_passes(st, sarena, fr, res, sig, passes, a.batch)
 
 
 kernel_rate(100)
