@@ -26,7 +26,9 @@
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <unistd.h>
+#include <atomic>
 #include <random>
+#include <thread>
 #include <vector>
 
 /* ---- stand-in for the GPU half (driver only) ---- */
@@ -50,7 +52,18 @@ static int stand_in_verify( uint8_t const * arena, uint64_t arena_sz, fd_ed25519
   return FD_ED25519_GPU_OK;
 }
 
-struct fd_ed25519_gpu { int8_t * pend_out; std::vector<int8_t> codes; int pend; };
+/* The device-parse queue's stand-in (devcap != 0): fd_ed25519_gpu_frags_submit
+   parses the frags with the host parser, verifies with the stand-in codes
+   and folds them per frag as the GPU's phase C does (the first error that is
+   not ERR_MSG, else ERR_MSG, else SUCCESS); the results reach the caller's
+   arrays only at the poll that completes the batch, after a few PENDING
+   answers to non-blocking polls -- the asynchronous discipline the stage's
+   poller and replayer threads run against. */
+struct fq_ent { int8_t * status; uint64_t * tag; std::vector<int8_t> s; std::vector<uint64_t> t; int spins; };
+struct fd_ed25519_gpu {
+  int8_t * pend_out; std::vector<int8_t> codes; int pend;
+  int devcap; fq_ent q[ FD_ED25519_GPU_QUEUE_DEPTH ]; int qh, qn; uint64_t submits, pending_polls, kicks;
+};
 
 extern "C" {
 int fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
@@ -68,12 +81,43 @@ int fd_ed25519_gpu_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64
 }
 int fd_ed25519_gpu_poll( fd_ed25519_gpu_t * ctx ) { if( ctx->pend ) ctx->pend--; return FD_ED25519_GPU_OK; }
 int fd_ed25519_gpu_poll_block( fd_ed25519_gpu_t * ctx ) { return fd_ed25519_gpu_poll( ctx ); }
-uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx ) { (void)ctx; return 0u; }   /* host parse only */
-int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n ) { (void)ctx; (void)n; return FD_ED25519_GPU_ERR_ARG; }
-int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t *, uint8_t const *, uint64_t, fd_ed25519_gpu_frag_t const *, uint64_t,
-                                 int8_t *, uint64_t * ) { return FD_ED25519_GPU_ERR_ARG; }
-int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t *, int ) { return FD_ED25519_GPU_OK; }
-int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t *, int ) { return FD_ED25519_GPU_OK; }
+uint64_t fd_ed25519_gpu_frags_cap( fd_ed25519_gpu_t const * ctx ) { return ctx->devcap ? 4096u : 0u; }
+int fd_ed25519_gpu_frags_reserve( fd_ed25519_gpu_t * ctx, uint64_t n ) {
+  return ctx->devcap && n <= 4096u ? FD_ED25519_GPU_OK : FD_ED25519_GPU_ERR_ARG;
+}
+int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, uint64_t arena_sz,
+                                 fd_ed25519_gpu_frag_t const * frag, uint64_t n, int8_t * status, uint64_t * tag ) {
+  if( !ctx->devcap || n > 4096u ) return FD_ED25519_GPU_ERR_ARG;
+  if( ctx->qn == FD_ED25519_GPU_QUEUE_DEPTH ) return FD_ED25519_GPU_ERR_BUSY;
+  fq_ent & e = ctx->q[ (ctx->qh + ctx->qn) % FD_ED25519_GPU_QUEUE_DEPTH ];
+  e.s.assign( n, 0 ); e.t.assign( n, 0u );
+  std::vector<fd_ed25519_desc_t> desc( 16u * n + 1u );
+  int64_t nd = fd_ed25519_gpu_frags_to_descs( arena, arena_sz, frag, n, desc.data(), desc.size(), e.s.data(), e.t.data() );
+  if( nd < 0 ) return (int)nd;
+  std::vector<int8_t> code( (size_t)nd + 1u );
+  int err = stand_in_verify( arena, arena_sz, desc.data(), (uint64_t)nd, code.data() );
+  if( err ) return err;
+  std::vector<int8_t> first( n, 0 ), any_msg( n, 0 );
+  for( int64_t k=0; k<nd; k++ ) {                          /* descriptors are in frag order (txn_idx: n <= 4096 here) */
+    uint16_t i = desc[ k ].txn_idx;
+    if( code[ k ] == FD_ED25519_ERR_MSG ) any_msg[ i ] = 1;
+    else if( code[ k ] != FD_ED25519_SUCCESS && !first[ i ] ) first[ i ] = code[ k ];
+  }
+  for( uint64_t i=0; i<n; i++ )
+    if( !e.s[ i ] ) e.s[ i ] = first[ i ] ? first[ i ] : (any_msg[ i ] ? (int8_t)FD_ED25519_ERR_MSG : (int8_t)FD_ED25519_SUCCESS);
+  e.status = status; e.tag = tag; e.spins = (int)(ctx->submits++ % 3u);
+  ctx->qn++;
+  return FD_ED25519_GPU_OK;
+}
+int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t * ctx, int block ) {
+  if( !ctx->qn ) return FD_ED25519_GPU_OK;
+  fq_ent & e = ctx->q[ ctx->qh ];
+  if( !block && e.spins > 0 ) { e.spins--; ctx->pending_polls++; return FD_ED25519_GPU_PENDING; }
+  for( size_t i=0; i<e.s.size(); i++ ) { e.status[ i ] = e.s[ i ]; e.tag[ i ] = e.t[ i ]; }
+  ctx->qh = (ctx->qh + 1) % FD_ED25519_GPU_QUEUE_DEPTH; ctx->qn--;
+  return FD_ED25519_GPU_OK;
+}
+int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t * ctx, int ) { ctx->kicks++; return FD_ED25519_GPU_OK; }
 int fd_ed25519_gpu_host_register_auto( fd_ed25519_gpu_t *, void *, uint64_t ) { return 1; }   /* "the caller's" */
 int fd_ed25519_gpu_host_unregister( fd_ed25519_gpu_t *, void * ) { return FD_ED25519_GPU_OK; }
 /* the shred path's GPU half: reads every byte the root kernel would (leaf,
@@ -136,7 +180,7 @@ static void rand_frag( std::vector<uint8_t> & a, std::vector<fd_ed25519_gpu_frag
   fr.push_back( { (uint32_t)off, (uint32_t)sz } );
 }
 
-static uint64_t st_desc, st_ok, st_failed, st_bad, st_walk, st_pub, st_avail, st_join_refused;
+static uint64_t st_desc, st_ok, st_failed, st_bad, st_walk, st_pub, st_avail, st_join_refused, st_devp, st_kicks;
 
 static void check_frags( int iters ) {
   for( int it=0; it<iters; it++ ) {
@@ -163,8 +207,61 @@ static void check_frags( int iters ) {
   }
 }
 
+/* The async stage with the frags parsed on the "GPU" (the stand-in queue
+   above) against the same stage with the host parse, batch for batch over
+   the same frags, each with its own tcache: equal results and signatures. */
+static void check_stage_device_parse( int iters ) {
+  for( int threads=1; threads<=3; threads += 2 ) {
+    fd_ed25519_gpu_t cd = {}, ch = {}; cd.devcap = 1;
+    fd_ed25519_gpu_tcache_t * td = fd_ed25519_gpu_tcache_new( 16, 64 );
+    fd_ed25519_gpu_tcache_t * th = fd_ed25519_gpu_tcache_new( 16, 64 );
+    fd_ed25519_gpu_stage_t * sd = fd_ed25519_gpu_stage_new( &cd, td, 64, threads );
+    fd_ed25519_gpu_stage_t * sh = fd_ed25519_gpu_stage_new( &ch, th, 64, threads );
+    if( !sd || !sh || fd_ed25519_gpu_stage_set_device_parse( sh, 0 ) ) { fprintf( stderr, "stage_new\n" ); exit( 1 ); }
+    std::vector<exact *> keep; std::vector<std::vector<fd_ed25519_gpu_frag_t> *> kf;
+    std::vector<std::vector<int8_t> *> kr[ 2 ]; std::vector<std::vector<uint64_t> *> ks[ 2 ];
+    /* a monitor thread reading the stages' counters while batches flow (a
+       counter updated outside the stage's lock is a ThreadSanitizer report) */
+    std::atomic<int> done( 0 );
+    std::thread mon( [&]{
+      fd_ed25519_gpu_stage_stats_t x;
+      while( !done.load() ) { fd_ed25519_gpu_stage_stats( sd, &x ); fd_ed25519_gpu_stage_stats( sh, &x ); std::this_thread::yield(); }
+    } );
+    for( int it=0; it<iters; it++ ) {
+      std::vector<uint8_t> a; auto * fr = new std::vector<fd_ed25519_gpu_frag_t>();
+      uint64_t n = 1 + rnd( 64 );
+      for( uint64_t i=0; i<n; i++ ) rand_frag( a, *fr );
+      auto * ar = new exact( a );
+      keep.push_back( ar ); kf.push_back( fr );
+      for( int m=0; m<2; m++ ) {
+        fd_ed25519_gpu_stage_t * st = m ? sh : sd;
+        auto * res = new std::vector<int8_t>( n, 99 ); auto * sig = new std::vector<uint64_t>( n, 0u );
+        kr[ m ].push_back( res ); ks[ m ].push_back( sig );
+        int e;
+        while( (e = fd_ed25519_gpu_stage_submit( st, ar->p, ar->n, fr->data(), n, res->data(), sig->data() )) == FD_ED25519_GPU_ERR_BUSY )
+          if( fd_ed25519_gpu_stage_poll( st, 1 ) ) { fprintf( stderr, "poll\n" ); exit( 1 ); }
+        if( e ) { fprintf( stderr, "submit %d\n", e ); exit( 1 ); }
+      }
+    }
+    for( fd_ed25519_gpu_stage_t * st : { sd, sh } )
+      while( fd_ed25519_gpu_stage_pending( st ) ) if( fd_ed25519_gpu_stage_poll( st, 1 ) ) { fprintf( stderr, "poll\n" ); exit( 1 ); }
+    done.store( 1 ); mon.join();
+    fd_ed25519_gpu_stage_delete( sd ); fd_ed25519_gpu_stage_delete( sh );
+    for( size_t b=0; b<keep.size(); b++ ) {
+      if( *kr[ 0 ][ b ] != *kr[ 1 ][ b ] || *ks[ 0 ][ b ] != *ks[ 1 ][ b ] ) {
+        fprintf( stderr, "device-parse stage differs from the host-parse stage at batch %zu\n", b ); exit( 1 );
+      }
+      delete keep[ b ]; delete kf[ b ];
+      for( int m=0; m<2; m++ ) { delete kr[ m ][ b ]; delete ks[ m ][ b ]; }
+    }
+    if( !cd.submits || !cd.pending_polls ) { fprintf( stderr, "device-parse queue not exercised\n" ); exit( 1 ); }
+    st_devp += cd.submits; st_kicks += cd.kicks;
+    fd_ed25519_gpu_tcache_delete( td ); fd_ed25519_gpu_tcache_delete( th );
+  }
+}
+
 static void check_stage( int iters ) {
-  fd_ed25519_gpu_t ctx; ctx.pend = 0;
+  fd_ed25519_gpu_t ctx = {}; ctx.pend = 0;
   fd_ed25519_gpu_tcache_t * tc = fd_ed25519_gpu_tcache_new( 16, 64 );
   for( int it=0; it<iters; it++ ) {                         /* sync stage */
     std::vector<uint8_t> a; std::vector<fd_ed25519_gpu_frag_t> fr;
@@ -454,6 +551,7 @@ int main( int argc, char ** argv ) {
   int scale = argc > 1 ? atoi( argv[ 1 ] ) : 1;
   check_frags( 3000 * scale );
   check_stage( 400 * scale );
+  check_stage_device_parse( 200 * scale );
   check_tcache( 20000 * scale );
   check_precompile( 3000 * scale );
   check_gossip( 3000 * scale );
@@ -461,9 +559,9 @@ int main( int argc, char ** argv ) {
   check_offload( 20000 * scale );
   printf( "sanitize_host: ok (frags: %lu parsed ok, %lu failed, %lu bad, %lu descriptors; precompile %lu descriptors; "
           "gossip %lu descriptors; crds %lu descriptors; shreds %lu descriptors; link %lu published, %lu taken, "
-          "%lu joins refused)\n",
+          "%lu joins refused; device-parse stage %lu batches, %lu kicks)\n",
           (unsigned long)st_ok, (unsigned long)st_failed, (unsigned long)st_bad, (unsigned long)st_desc, (unsigned long)st_walk,
           (unsigned long)st_gossip, (unsigned long)st_crds, (unsigned long)st_shred, (unsigned long)st_pub,
-          (unsigned long)st_avail, (unsigned long)st_join_refused );
+          (unsigned long)st_avail, (unsigned long)st_join_refused, (unsigned long)st_devp, (unsigned long)st_kicks );
   return 0;
 }

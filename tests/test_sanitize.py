@@ -1,4 +1,4 @@
-"""CPU: AddressSanitizer + UndefinedBehaviorSanitizer over the host code that
+"""CPU: AddressSanitizer + UndefinedBehaviorSanitizer (and ThreadSanitizer) over the host code that
 parses attacker-shaped bytes: the frag ->
 descriptor parse, the tcache, the sync and async verify stages (host parse),
 the precompile record walk, the gossip packet walks (CRDS values included), the shred walk and the
@@ -37,6 +37,19 @@ def test_sanitized_driver():
     nums = [int(x) for x in re.findall(r"(\d+) (?:parsed ok|failed|bad|descriptors|published|taken|joins refused)",
                                         r.stdout)]
     assert len(nums) == 11 and min(nums) > 0, r.stdout
+    m = re.search(r"device-parse stage (\d+) batches, (\d+) kicks", r.stdout)
+    assert m and int(m.group(1)) > 0 and int(m.group(2)) > 0, r.stdout
+
+
+def test_thread_sanitized_driver():
+    """The same driver under ThreadSanitizer: the async stage's three threads
+    (caller, poller, replayer) on the host-parse and the device-parse paths,
+    the stand-in device queue answering PENDING and taking drain kicks."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "tests", "csrc"), "tsan"])
+    r = subprocess.run([os.path.join(BUILD, "tsan_host")], capture_output=True, text=True, timeout=900,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "sanitize_host: ok" in r.stdout and "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
 
 
 def test_cpu_suites_against_asan_libraries():
