@@ -18,6 +18,8 @@
 #   tools/gpu.sh abstage "A:" "B:ENV=v" same-process A/B of stage settings (tools/ab_stage.py)
 #   tools/gpu.sh clock 2|3              in-kernel clock stamps of config 2 / 3 (stamps build)
 #   tools/gpu.sh crashctl MODE          exit-SIGSEGV control run (tools/crash_control.py) under the trace flags
+#   tools/gpu.sh box                    the box's GPU: serial, power cap and draw, temperatures, clocks
+#                                       (read-only rocm-smi / amd-smi queries) -> gpurun_out/box_$TAG.txt
 #   tools/gpu.sh run SECONDS CMD...     any other command under its own time limit
 set -e
 mkdir -p gpurun_out
@@ -106,6 +108,10 @@ case "$cmd" in
   abstage)
     timeout -k 10 600 python3 -u tools/ab_stage.py "$@" > gpurun_out/abstage_$T.log 2>&1 || { tail -20 gpurun_out/abstage_$T.log; exit 1; }
     grep -v amdgpu.ids gpurun_out/abstage_$T.log ;;
+  box)
+    { timeout -k 10 60 rocm-smi --showserial -M -P -t -c; timeout -k 10 60 amd-smi static --limit; } \
+      > gpurun_out/box_$T.txt 2>&1 || true
+    grep -v "^$" gpurun_out/box_$T.txt | grep -iv "warning" | head -80 ;;
   run)
     lim=$1; shift
     timeout -k 10 $lim "$@" ;;
