@@ -187,6 +187,8 @@ def main():
             per = lambda ns: ns / args.steps / 1e6          # ms per run
             out[mode] = {
                 "frags_per_s": args.frags / dt_m, "sigs_per_s": n_sigs / dt_m, "ms": dt_m * 1e3,
+                "runs": len(t), "sigs_per_s_median": n_sigs / float(np.median(t)),
+                "sigs_per_s_min_max": [n_sigs / max(t), n_sigs / min(t)],
                 "caller_ms_per_run": {"submit": calls["submit_s"] / args.steps * 1e3,
                                       "poll_wait": calls["poll_s"] / args.steps * 1e3},
                 "stage_ms_per_run": {k[:-3]: per(v) for k, v in st.items() if k.endswith("_ns")},

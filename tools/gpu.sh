@@ -71,7 +71,7 @@ case "$cmd" in
   stage)
     timeout -k 10 400 python3 -u tools/bench_verify_stage.py ${@:---frags 1048576 --steps 5 --warmup 1 --no-cpu --async-batch 36000} \
       > gpurun_out/stage_$T.json 2> gpurun_out/stage_$T.err || { tail -20 gpurun_out/stage_$T.err; exit 1; }
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); a=d['async_device_parse']; print('reg %.1f M sigs/s, pageable %.1f M sigs/s, streaming %.1f M sigs/s' % (a['registered']['sigs_per_s']/1e6, a['pageable']['sigs_per_s']/1e6, a['streaming']['sigs_per_s']/1e6))" gpurun_out/stage_$T.json ;;
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); a=d['async_device_parse']; r=a['registered']; print('reg %.1f M sigs/s (median of %d runs %.1f, %.1f-%.1f), pageable %.1f M sigs/s, streaming %.1f M sigs/s' % (r['sigs_per_s']/1e6, r['runs'], r['sigs_per_s_median']/1e6, r['sigs_per_s_min_max'][0]/1e6, r['sigs_per_s_min_max'][1]/1e6, a['pageable']['sigs_per_s']/1e6, a['streaming']['sigs_per_s']/1e6))" gpurun_out/stage_$T.json ;;
   stagetrace)
     cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
     timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/stagetr_$T -o tr -- \
