@@ -16,6 +16,11 @@ leave.  Algorithmic bytes come from the kernel's layout
 and the digit distribution of the batch's scalars.
 
   python3 tools/byte_ledger.py bytes_ledger.jsonl [--n 65536] [--out ledger.json]
+
+The builds (tools/bin is scratch; rebuild them from the tree):
+  tools/build_var.sh prod5="" notail5="-DFD_DIAG_VTAB_NO_TAIL" \
+      onee5="-DFD_DIAG_VTAB_ONE_ENTRY" nostore5="-DFD_DIAG_NO_VTAB_STORE" comb1_5="-DFD_DIAG_COMB_POS=1"
+  gpurun ... 'AB_NOCHECK=1 TAG=ledger tools/gpu.sh bytes tools/bin/libvar_{prod5,notail5,onee5,nostore5,comb1_5}.so'
 """
 import argparse
 import json
