@@ -20,6 +20,9 @@
 #   tools/gpu.sh crashctl MODE          exit-SIGSEGV control run (tools/crash_control.py) under the trace flags
 #   tools/gpu.sh box                    the box's GPU: serial, power cap and draw, temperatures, clocks
 #                                       (read-only rocm-smi / amd-smi queries) -> gpurun_out/box_$TAG.txt
+#   tools/gpu.sh power [bench args]     bench.py in the background; rocm-smi power / clock samples every
+#                                       0.4 s and one amd-smi metric dump once it draws > 1 kW
+#                                       -> gpurun_out/power_$TAG.txt, amdsmi_$TAG.txt, bench_$TAG.json
 #   tools/gpu.sh run SECONDS CMD...     any other command under its own time limit
 set -e
 mkdir -p gpurun_out
@@ -112,6 +115,23 @@ case "$cmd" in
     { timeout -k 10 60 rocm-smi --showserial -M -P -t -c; timeout -k 10 60 amd-smi static --limit; } \
       > gpurun_out/box_$T.txt 2>&1 || true
     grep -v "^$" gpurun_out/box_$T.txt | grep -iv "warning" | head -80 ;;
+  power)
+    : > gpurun_out/power_$T.txt
+    timeout -k 10 300 python3 bench.py --no-cpu "$@" > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err &
+    P=$!; n=0
+    for i in $(seq 1 600); do
+      sleep 0.4
+      kill -0 $P 2>/dev/null || break
+      echo "T$i" >> gpurun_out/power_$T.txt
+      timeout -k 5 20 rocm-smi -P -c -t >> gpurun_out/power_$T.txt 2>&1 || true
+      w=$(tail -25 gpurun_out/power_$T.txt | grep -oE "Power \(W\): [0-9.]+" | tail -1 | awk '{print int($3)}')
+      if [ -n "$w" ] && [ "$w" -gt 1000 ]; then
+        n=$((n+1)); [ $n = 6 ] && { timeout -k 5 30 amd-smi metric > gpurun_out/amdsmi_$T.txt 2>&1 || true; }
+      fi
+    done
+    wait $P
+    grep -E "SOCKET_POWER|PPT_VIOLATION_ACTIVITY" gpurun_out/amdsmi_$T.txt 2>/dev/null || true
+    tail -c 300 gpurun_out/bench_$T.json ;;
   run)
     lim=$1; shift
     timeout -k 10 $lim "$@" ;;
