@@ -14,7 +14,7 @@ raises otherwise.
 from .ed25519 import (  # noqa: F401
     FD_ED25519_SUCCESS, FD_ED25519_ERR_SIG, FD_ED25519_ERR_PUBKEY, FD_ED25519_ERR_MSG,
     CODES_AVX512, CODES_REF, DESC_DTYPE, PRECOMPILE_DTYPE, SPAN_DTYPE, SHA_MSG_DTYPE, Ed25519Gpu, GpuError, lib_path, load_lib, pack_batch,
-    strerror, txn_reduce, ctab_stats, build_id, gossip_walk, gossip_walk_crds, GOSSIP_CORRUPT, GOSSIP_UNSIGNED, GOSSIP_NOT_MINE, GOSSIP_CRDS,
+    strerror, txn_reduce, ctab_stats, build_id, runtime_info, host_is_registered, gossip_walk, gossip_walk_crds, GOSSIP_CORRUPT, GOSSIP_UNSIGNED, GOSSIP_NOT_MINE, GOSSIP_CRDS,
     QUEUE_DEPTH,
     STAGE_DEPTH,
     GOSSIP_NO_VALUES,

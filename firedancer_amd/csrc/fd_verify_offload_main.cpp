@@ -67,6 +67,7 @@ int main( int argc, char ** argv ) {
   uint8_t * dc = fd_verify_offload_dcache( off );
   int pinned = !fd_ed25519_gpu_host_register( ctx, dc, fd_verify_offload_dcache_sz( off ) );
   fprintf( stderr, "fd_verify_offload_server: frag area %s\n", pinned ? "page-locked" : "pageable (register failed)" );
+  fprintf( stderr, "fd_verify_offload_server: runtime %s, library %s\n", fd_ed25519_gpu_runtime(), fd_ed25519_gpu_build_id() );
   fprintf( stderr, "fd_verify_offload_server: serving %s (depth %lu, frag area %lu MB, batch %lu)\n",
            name, (unsigned long)depth, (unsigned long)dcache_mb, (unsigned long)batch );
   fflush( stderr );

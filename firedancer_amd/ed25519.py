@@ -84,6 +84,9 @@ def load_lib():
     lib.fd_ed25519_gpu_launch_stats.argtypes = [vp, vp, vp]
     lib.fd_ed25519_gpu_build_id.restype = ctypes.c_char_p
     lib.fd_ed25519_gpu_build_id.argtypes = []
+    lib.fd_ed25519_gpu_runtime.restype = ctypes.c_char_p
+    lib.fd_ed25519_gpu_runtime.argtypes = []
+    lib.fd_ed25519_gpu_host_is_registered.argtypes = [vp, u64]
     lib.fd_ed25519_verify_batch_gpu_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_pipe_dev.argtypes = [vp, i32, vp, u64, vp, u64, vp, vp]
     lib.fd_ed25519_gpu_pipe_flush_dev.argtypes = [vp, i32, vp]
@@ -142,6 +145,18 @@ def build_id():
     """{"code": sha-256 prefix of the embedded code object, "git": describe of the built tree}"""
     s = load_lib().fd_ed25519_gpu_build_id().decode()
     return dict(kv.split("=", 1) for kv in s.split())
+
+
+def runtime_info():
+    """{"hip": path of the libamdhip64 the library's HIP calls resolve to, "version": hipRuntimeGetVersion}:
+    torch's bundled runtime when torch was imported first, /opt/rocm's otherwise (FD_ED25519_GPU_NO_TORCH=1)."""
+    s = load_lib().fd_ed25519_gpu_runtime().decode()
+    return dict(kv.split("=", 1) for kv in s.split())
+
+
+def host_is_registered(buf):
+    """fd_ed25519_gpu_host_is_registered: is the array page-locked (registered / hipHostMalloc'd)?"""
+    return load_lib().fd_ed25519_gpu_host_is_registered(_ptr(buf), buf.nbytes) == 1
 
 
 def ctab_stats(dev=0):

@@ -145,6 +145,14 @@ int fd_ed25519_verify_batch_gpu( fd_ed25519_gpu_t *        ctx,
 int fd_ed25519_gpu_host_register  ( fd_ed25519_gpu_t * ctx, void * p, uint64_t sz );
 int fd_ed25519_gpu_host_unregister( fd_ed25519_gpu_t * ctx, void * p );
 
+/* 1 if the HIP runtime knows [p, p + sz) as page-locked host memory (both
+   ends registered or hipHostMalloc'd), 0 if not.  The library asks this
+   before it page-locks a frag area itself (the async stage's opt-in autoreg,
+   the offload serve loop), so a range the caller registered keeps exactly
+   one owner: a second hipHostRegister of a registered range returns
+   success on ROCm 7.2, and one unregister would then drop it for both. */
+int fd_ed25519_gpu_host_is_registered( void const * p, uint64_t sz );
+
 /* Hot-key cache.  Solana traffic is dominated by a few thousand repeat
    signers (validators' vote authorities), so the context can keep, per
    cached public key A, a comb table of [j](256^p (-A)), p < 32, j <= 128
@@ -263,6 +271,13 @@ char const * fd_ed25519_gpu_strerror( int err );
    object> git=<git describe of the tree it was built from>": profiles
    (profiles/rNN/) record it, so a measurement can be matched to a build. */
 char const * fd_ed25519_gpu_build_id( void );
+
+/* "hip=<path of the libamdhip64 this process resolved the library's HIP
+   calls to> version=<hipRuntimeGetVersion>": a process that imported torch
+   first runs the library on torch's bundled runtime, a C program on
+   /opt/rocm's; tests and bench lines record which one they measured.  Does
+   not initialise the GPU beyond what the version query does. */
+char const * fd_ed25519_gpu_runtime( void );
 
 /* Batched SHA-512 (replaces fd_sha512_batch_init/_add/_fini,
    src/ballet/sha512/fd_sha512.h:223-408, i.e. fd_sha512_hash per message,

@@ -56,6 +56,31 @@ def ref_seq(ref, arena, frags, depth=16, map_cnt=64):
     return res[:len(frags)], tag[:len(frags)]
 
 
+def ref_seq_stream(ref, arena, batches, depth=16, map_cnt=64):
+    """The reference tile over batches fed in arrival order through one tcache
+    (their concatenation).  Frags lying past the arena (the tests' BAD_FRAG
+    runs: off = len(arena) + 64) would make the reference read outside it; the
+    tile rejects them before any tcache step (fd_verify.c:94-115), so they are
+    BAD_FRAG with tag 0 and the reference runs over the rest."""
+    allf = np.concatenate(batches)
+    inside = (allf["off"].astype(np.int64) + allf["sz"]) <= len(arena)
+    res = np.full(len(allf), BAD, np.int8)
+    tag = np.zeros(len(allf), np.uint64)
+    r, t = ref_seq(ref, arena, allf[inside], depth, map_cnt)
+    res[inside], tag[inside] = r, t
+    out, k = [], 0
+    for b in batches:
+        out.append((res[k:k + len(b)], tag[k:k + len(b)]))
+        k += len(b)
+    return out
+
+
+def assert_vs_ref(got_res, got_tag, exp, what):
+    for k, ((gr, gt), (er, et)) in enumerate(zip(zip(got_res, got_tag), exp)):
+        bad = np.nonzero((gr != er) | (gt != et))[0]
+        assert len(bad) == 0, (what, k, [(int(j), int(gr[j]), int(er[j])) for j in bad[:10]])
+
+
 def fixture_txns():
     d = json.load(open(os.path.join(REPO, "tests", "golden", "verify_txns.json")))["txns"]
     return {k: (bytes.fromhex(v["payload"]), bytes.fromhex(v["txn_t"])) for k, v in d.items()}
@@ -542,6 +567,98 @@ def test_offload_link_served_on_gpu_vs_reference_tile(gpu, ref):
 
 
 @pytest.mark.gpu
+def test_offload_server_process_vs_reference_tile(ref):
+    """The offload server as the sandboxed tile would run it: the C binary
+    firedancer_amd/fd_verify_offload_server in a process of its own (no torch:
+    the HIP runtime it links, /opt/rocm's), this process only a client of the
+    shared-memory link (libfd_verify_offload.so, no HIP).  20,000 frags of a
+    random stream (near and far repeats, corrupted signatures and messages,
+    sanity failures) published in bursts; every result and opt_sig equals the
+    sequential reference tile's, the server exits 0 with its stats, and its
+    stderr has no failure line -- in particular no double hipHostUnregister of
+    the frag area main() page-locks and the serve loop no longer re-registers
+    (gpurun_out/offload_server_r05g.err)."""
+    import subprocess
+    import time
+    rng = np.random.default_rng(5150)
+    arena, frags = _random_frag_stream(rng, 3000, 20000)
+    exp_res, exp_tag = ref_seq(ref, arena, frags)
+    name = "/fdvo_srv_%d" % os.getpid()
+    err_path = os.path.join(REPO, "gpurun_out", "offload_server_test.err")
+    os.makedirs(os.path.dirname(err_path), exist_ok=True)
+    env = dict(os.environ)
+    env.pop("FD_ED25519_GPU_STAGE_AUTOREG", None)
+    with open(err_path, "w") as ef:
+        p = subprocess.Popen([fa.server_path(), "--name", name, "--batch", "4096", "--threads", "4",
+                              "--dcache-mb", "64", "--depth", "8192"],
+                             stdout=subprocess.PIPE, stderr=ef, env=env, text=True)
+    try:
+        line = p.stdout.readline()                        # {"ready": true} once the GPU is up and warm
+        assert "ready" in line, (line, open(err_path).read())
+        cli = fa.OffloadLink.join(name)
+        n = len(frags)
+        depth = cli.depth
+        res = np.zeros(n, np.int8)
+        sig = np.zeros(n, np.uint64)
+        fr = np.ascontiguousarray(frags)
+        pub = nxt = 0
+        t0 = time.time()
+        while nxt < n:
+            if pub < n:      # a result slot is reused when seq + depth is published: stay within depth of nxt
+                pub += cli.publish_burst(arena, fr[pub:min(n, nxt + depth)])
+            if nxt < pub:
+                nxt += cli.results(nxt, res[nxt:pub], sig[nxt:pub])
+            assert time.time() - t0 < 90, ("offload server stalled", nxt, pub)
+        cli.halt()
+        cli.close()
+        out, _ = p.communicate(timeout=60)
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    err = open(err_path).read()
+    assert p.returncode == 0, (p.returncode, out, err)
+    stats = json.loads(out.strip().splitlines()[-1])
+    assert stats["err"] == 0 and stats["frags"] == n and stats["batches"] > 4, stats
+    assert "failed" not in err, err
+    assert "runtime hip=" in err and "torch" not in err.split("runtime hip=")[1].split()[0], err
+    bad = np.nonzero((res != exp_res) | (sig != exp_tag))[0]
+    assert len(bad) == 0, [(int(j), int(res[j]), int(exp_res[j])) for j in bad[:10]]
+    hist = {int(k): int(v) for k, v in zip(*np.unique(exp_res, return_counts=True))}
+    assert hist.get(S, 0) > 3000 and hist.get(D, 0) > 1000 and hist.get(F, 0) > 1000 and hist.get(BAD, 0) > 100, hist
+
+
+@pytest.mark.gpu
+def test_stage_autoreg_keeps_callers_registration(gpu, monkeypatch):
+    """One owner per page-locked range: with the stage's opt-in autoreg on, a
+    frag area the caller registered itself stays registered after the stage
+    is deleted (the caller's own unregister succeeds), and an area the stage
+    registered is released by the stage.  (ROCm 7.2 answers a second
+    hipHostRegister of a registered range with success, so the library asks
+    the runtime first: fd_ed25519_gpu_host_is_registered.)"""
+    monkeypatch.setenv("FD_ED25519_GPU_STAGE_AUTOREG", "1")
+    fx = fixture_txns()
+    for caller_registers in (True, False):
+        arena, frags = _mk_frags([fx[k] for k in ["valid_txn_2sigs", "invalid_txn_same_1sig", "valid_txn_1sig"]])
+        arena = np.concatenate([arena, np.zeros(8192, np.uint8)])
+        if caller_registers:
+            gpu.host_register(arena)
+        assert fa.host_is_registered(arena) == caller_registers
+        ast = fa.AsyncStage(gpu, fa.TCache(), 64, threads=1, device_parse=True)
+        res = np.zeros(len(frags), np.int8); sig = np.zeros(len(frags), np.uint64)
+        ast.submit(arena, len(arena), np.ascontiguousarray(frags), res, sig)
+        while ast.pending():
+            ast.poll(True)
+        assert fa.host_is_registered(arena)               # registered while the stage holds it
+        ast.close()
+        assert list(res) == [S, F, S]
+        assert fa.host_is_registered(arena) == caller_registers
+        if caller_registers:
+            gpu.host_unregister(arena)                    # raises if the stage had dropped it
+        assert not fa.host_is_registered(arena)
+
+
+@pytest.mark.gpu
 def test_stage_device_parse_bad_frags(gpu):
     """The device parse classifies every sanity failure as the host parse
     does -- including a frag claiming more signatures than it can hold,
@@ -681,7 +798,7 @@ def test_stage_device_parse_many_workgroups(gpu, n):
 
 
 @pytest.mark.gpu
-def test_stage_in_launch_parse_vs_parse_launch(monkeypatch):
+def test_stage_in_launch_parse_vs_parse_launch(monkeypatch, ref):
     """The pipelined path's in-launch parse (the verify launch's phase-A waves
     parse the batch's frags, look-back scan and all, then wait for the tiles
     holding their descriptors) against a parse launch first
@@ -726,13 +843,15 @@ def test_stage_in_launch_parse_vs_parse_launch(monkeypatch):
     for k in range(len(batches)):
         bad = np.nonzero((out["1"][0][k] != out["0"][0][k]) | (out["1"][1][k] != out["0"][1][k]))[0]
         assert len(bad) == 0, (k, [(int(j), int(out["1"][0][k][j]), int(out["0"][0][k][j])) for j in bad[:10]])
+    exp = ref_seq_stream(ref, arena_u, batches)           # and both against the reference tile
+    assert_vs_ref(out["1"][0], out["1"][1], exp, "in-launch parse")
     hist = {int(c): int(v) for c, v in zip(*np.unique(out["1"][0][0], return_counts=True))}
     assert hist.get(S, 0) > 1000 and hist.get(BAD, 0) > 3000, hist
     assert np.all(out["1"][0][2] == BAD)
 
 
 @pytest.mark.gpu
-def test_stage_in_launch_parse_two_contexts_concurrently():
+def test_stage_in_launch_parse_two_contexts_concurrently(ref):
     """Two contexts on one GPU, each with its own stage, fed from two threads
     at once: their pipelined verify launches share the CUs, so a launch's
     workgroups are not all resident together.  The in-launch parse takes its
@@ -787,13 +906,15 @@ def test_stage_in_launch_parse_two_contexts_concurrently():
             for j in range(len(streams[k])):
                 assert np.array_equal(out["alone"][0][k][j], out["together"][0][k][j]), (k, j)
                 assert np.array_equal(out["alone"][1][k][j], out["together"][1][k][j]), (k, j)
+            exp = ref_seq_stream(ref, arena_u, streams[k])   # each stream against the reference tile
+            assert_vs_ref(out["together"][0][k], out["together"][1][k], exp, "stream %d" % k)
     finally:
         for g in ctxs:
             g.close()
 
 
 @pytest.mark.gpu
-def test_stage_in_launch_parse_small_signature_bound(monkeypatch):
+def test_stage_in_launch_parse_small_signature_bound(monkeypatch, ref):
     """A pipelined frag batch whose host-side signature bound is tiny (30,000
     64-byte junk frags bound no signature) but whose parse has 118 tiles:
     the launch still gets a workgroup per tile to parse them, and the valid
@@ -820,4 +941,10 @@ def test_stage_in_launch_parse_small_signature_bound(monkeypatch):
             g.close()
         out[ap] = (res, sig)
     assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
+    # no junk frag verifies (most are BAD_FRAG: their fd_txn_t would lie outside the
+    # frag, DESIGN §7's documented rule), so none inserts into the tcache; the valid
+    # frags behind them then give the reference tile's results over those frags alone
+    assert not np.any(out["1"][0][:len(junk)] == S)
+    er, et = ref_seq(ref, arena_u, batch[len(junk):])
+    assert_vs_ref([out["1"][0][len(junk):]], [out["1"][1][len(junk):]], [(er, et)], "valid frags behind junk")
     assert np.count_nonzero(out["1"][0][len(junk):] == S) > 50
