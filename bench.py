@@ -321,6 +321,109 @@ def hostfed_main(args):
     return 0
 
 
+def notorch_main(args):
+    """--path no-torch: the headline config-2 step (device-resident 64K x 200 B, one
+    fd_ed25519_gpu_pipe_dev launch per step, codes checked after the run) with NO
+    torch in the process: device memory, the stream and the timing events come
+    from the HIP runtime the library links (/opt/rocm), through ctypes -- the
+    runtime the C product (offload server, a C verify tile) runs on.  The
+    headline line runs on torch's bundled runtime (torch imported first); this
+    line puts the two side by side (VERDICT r05 #7).  N=1, a line of its own."""
+    os.environ["FD_ED25519_GPU_NO_TORCH"] = "1"
+    import firedancer_amd as fa
+    fa.load_lib()
+    hip = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
+    vp, sz_t = ctypes.c_void_p, ctypes.c_size_t
+    n = args.batch or 65536
+    assert n <= 65536, "--path no-torch runs the pipelined config-2 step (at most one wave per SIMD)"
+    arena, desc, sz, expect, data_desc = build_workload(n, args.msg_sz, seed=0)
+    assert hip.hipSetDevice(0) == 0
+
+    def dmalloc(nb):
+        p = vp()
+        assert hip.hipMalloc(ctypes.byref(p), sz_t(nb)) == 0
+        return p.value
+
+    def h2d(d, a):
+        assert hip.hipMemcpy(vp(d), vp(a.ctypes.data), sz_t(a.nbytes), 1) == 0
+
+    d_arena, d_desc = dmalloc(arena.nbytes), dmalloc(desc.nbytes)
+    h2d(d_arena, arena)
+    h2d(d_desc, np.ascontiguousarray(desc))
+    d_outs = [dmalloc(n), dmalloc(n)]
+    stream = vp()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(stream), 1) == 0      # non-blocking, like torch's side stream
+    g = fa.Ed25519Gpu(device_mask=1, max_batch=n)
+    nstep = [0]
+
+    def step():
+        g.pipe_dev(d_arena, sz, d_desc, n, d_outs[nstep[0] & 1], stream=stream.value)
+        nstep[0] += 1
+
+    def sync():
+        assert hip.hipStreamSynchronize(stream) == 0
+
+    def event():
+        e = vp()
+        assert hip.hipEventCreate(ctypes.byref(e)) == 0
+        return e
+
+    def elapsed(a, b):
+        ms = ctypes.c_float(0)
+        assert hip.hipEventElapsedTime(ctypes.byref(ms), a, b) == 0
+        return ms.value
+
+    prime, t_prime = 0, time.perf_counter()
+    while (time.perf_counter() - t_prime) * 1e3 < args.prime_ms:
+        for _ in range(8):
+            step()
+        prime += 8
+        sync()
+    for _ in range(args.warmup):
+        step()
+    sync()
+    ev0, ev1 = event(), event()
+    t0 = time.perf_counter()
+    hip.hipEventRecord(ev0, stream)
+    for _ in range(args.steps):
+        step()
+    hip.hipEventRecord(ev1, stream)
+    sync()
+    dt = time.perf_counter() - t0
+    region_ms = elapsed(ev0, ev1) / args.steps
+    evs = [(event(), event()) for _ in range(min(args.steps, 50))]
+    for a, b in evs:
+        hip.hipEventRecord(a, stream)
+        step()
+        hip.hipEventRecord(b, stream)
+    sync()
+    launch_ms = float(np.mean([elapsed(a, b) for a, b in evs]))
+    g.pipe_flush_dev(stream=stream.value)
+    sync()
+    for d in d_outs:
+        o = np.zeros(n, np.int8)
+        assert hip.hipMemcpy(vp(o.ctypes.data), vp(d), sz_t(n), 2) == 0
+        assert np.array_equal(o, expect), "verify codes differ from the expected ones"
+    value = n * args.steps / dt
+    peak = valu_peak()
+    line = {"metric": "Ed25519 verifies/sec (no torch in the process)", "value": value, "unit": "verifies/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "dtype": "u32", "data": "synthetic: " + data_desc,
+            "config": {"workload": "config2: %d-signature batch, fixed %d-B messages, device-resident" % (n, args.msg_sz),
+                       "batch_per_gpu": n},
+            "roofline": {"bound": "valu-int32", "achieved": W_MAC * value / 1e12, "peak": peak / 1e12,
+                         "frac": W_MAC * value / peak, "region_ms_per_launch": region_ms, "kernel_ms": launch_ms,
+                         "kernel_frac": W_MAC * n / (launch_ms * 1e-3) / peak},
+            "warmup_detail": {"prime_steps": prime, "warmup_steps": args.warmup},
+            "build": fa.build_id(), "runtime": fa.runtime_info(), "torch_loaded": "torch" in sys.modules}
+    g.close()
+    for d in [d_arena, d_desc] + d_outs:
+        hip.hipFree(vp(d))
+    hip.hipStreamDestroy(stream)
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def shred_main(args):
     """--path shred: shreds/s through fd_ed25519_gpu_shred_verify (the
     FEC resolver's first-shred check as a descriptor source, SURVEY.md §8(f)).
@@ -448,14 +551,15 @@ def main():
                          "fd_ed25519_gpu_verify_batch_dev launch (the whole batch); -1 (default): 1 when the batch "
                          "is at most one wave per SIMD (256 x CUs signatures: config 2), else 0 (larger batches "
                          "already give every SIMD several waves, and the single-lane kernel packs them better)")
-    ap.add_argument("--path", default="verify", choices=["verify", "shred", "host-fed"],
+    ap.add_argument("--path", default="verify", choices=["verify", "shred", "host-fed", "no-torch"],
                     help="verify (default): the headline line above.  shred: the FEC resolver's first-shred check "
                          "(fd_ed25519_gpu_shred_verify: host walk, Merkle roots on the GPU, verify) over the "
                          "reference's demo capture tiled to --batch, from host memory, N=1; a line of its own "
                          "(not the headline metric) with the host-hash variant and the reference's one-core check "
                          "(oracle/_ref fdref_shred_check) beside it.  host-fed: configs 2 and 3 from HOST memory "
                          "(sync calls and the async submit/poll stream, pageable and page-locked) beside the H2D "
-                         "bandwidth, N=1, a line of its own")
+                         "bandwidth, N=1, a line of its own.  no-torch: the config-2 step with no torch in the "
+                         "process (device memory, stream and events from the library's own HIP runtime), N=1")
     ap.add_argument("--stub", action="store_true",
                     help="CPU test mode (tests/test_bench_launch.py): gloo, a no-op step on a fixed count; "
                          "exercises the launcher, rank setup and SUM/MAX aggregation without a GPU")
@@ -481,6 +585,11 @@ def main():
             print("bench.py: --path host-fed runs on one GPU", file=sys.stderr, flush=True)
             sys.exit(2)
         sys.exit(hostfed_main(args))
+    if args.path == "no-torch":
+        if world != 1:
+            print("bench.py: --path no-torch runs on one GPU", file=sys.stderr, flush=True)
+            sys.exit(2)
+        sys.exit(notorch_main(args))
 
     import torch
     import torch.distributed as dist
@@ -641,6 +750,7 @@ def main():
                               "note": "prime steps run back to back for prime_ms first (the clock ramps from idle), "
                                       "then the warmup steps; none of them is timed"},
             "build": build,
+            "runtime": fa.runtime_info(),
         }
         if pipe:
             line["pipeline"] = {

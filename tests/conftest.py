@@ -41,3 +41,25 @@ def gpu():
     g = fa.Ed25519Gpu(device_mask=1, max_batch=1 << 16)
     yield g
     g.close()
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """Which HIP runtime the library ran on in this process (torch's bundled one when
+    torch was imported first, /opt/rocm's otherwise; fd_ed25519_gpu_runtime), also
+    written to gpurun_out/tests_runtime.json for the round's records."""
+    try:
+        import json
+        import firedancer_amd.ed25519 as e
+        if e._LIB is None:
+            return
+        info = {"runtime": e.runtime_info(), "build": e.build_id(), "torch_loaded": "torch" in sys.modules,
+                "markexpr": config.getoption("markexpr", "")}
+    except Exception:      # noqa: BLE001 -- a summary line must never fail the run
+        return
+    terminalreporter.write_line("fd_ed25519_gpu runtime: %s (torch loaded: %s)" % (info["runtime"], info["torch_loaded"]))
+    try:
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", "tests_runtime.json"), "w") as f:
+            json.dump(info, f)
+    except OSError:
+        pass

@@ -629,6 +629,40 @@ def test_offload_server_process_vs_reference_tile(ref):
 
 
 @pytest.mark.gpu
+def test_stage_bench_shape_vs_reference_tile(ref):
+    """The stage bench's own shape (tools/bench_verify_stage.py): its stream
+    generator (1-4 signers, 10 % duplicates at short distances), 110,000 frags
+    cut continuously into 36,000-frag batches (three full pipelined batches of
+    ~64K signatures, one wave per SIMD each, and a remainder), the frags
+    parsed inside the verify launch (the default), the area page-locked like
+    the offload server's dcache.  Every result and opt_sig equals the
+    sequential reference tile's over the same stream."""
+    from bench_verify_stage import make_stream, stream_passes
+    arena, frags, n_sigs = make_stream(110000, 0.1, seed=11)
+    exp_res, exp_tag = ref_seq(ref, arena, frags)
+    g = fa.Ed25519Gpu(device_mask=1, max_batch=1 << 18)
+    try:
+        g.host_register(arena)
+        ast = fa.AsyncStage(g, fa.TCache(), 36000, threads=8, device_parse=True)
+        fr = np.ascontiguousarray(frags)
+        res = np.zeros(len(fr), np.int8)
+        sig = np.zeros(len(fr), np.uint64)
+        stream_passes(ast, arena, fr, res, sig, 1, 36000)
+        st = ast.stats()
+        ast.close()
+        pipe_l, one_l = g.launch_stats()
+        g.host_unregister(arena)
+    finally:
+        g.close()
+    assert st["batches"] == 4, st
+    assert pipe_l >= 4, (pipe_l, one_l)                   # the batches ran on the pipelined kernel
+    bad = np.nonzero((res != exp_res) | (sig != exp_tag))[0]
+    assert len(bad) == 0, [(int(j), int(res[j]), int(exp_res[j])) for j in bad[:10]]
+    hist = {int(k): int(v) for k, v in zip(*np.unique(exp_res, return_counts=True))}
+    assert hist.get(S, 0) > 90000 and hist.get(D, 0) > 5000, hist
+
+
+@pytest.mark.gpu
 def test_stage_autoreg_keeps_callers_registration(gpu, monkeypatch):
     """One owner per page-locked range: with the stage's opt-in autoreg on, a
     frag area the caller registered itself stays registered after the stage
