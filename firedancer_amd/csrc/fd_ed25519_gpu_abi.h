@@ -89,6 +89,11 @@ struct verify_args {
 /* A frag's result in the page-locked staging of the device frag path: one
    16-byte record, written by the device with one store. */
 typedef struct __attribute__(( aligned( 16 ) )) { uint32_t tag_lo, tag_hi; int32_t status; uint32_t pad; } fd_frec_t;
+/* The status the host writes into every record of a slot before the batch's
+   launch (no device status is ever this value): a record still holding it
+   when the batch's completion event has fired was never written (or not yet
+   visible), and the poll waits for it, then fails the batch. */
+#define FD_FREC_UNSET ((int32_t)0x80000000)
 
 /* Device-side frag parsing (verify stage, fd_verify_stage.cpp): the frags
    [off, off+sz) index a copy of the arena span [span_lo, span_lo+span_sz).

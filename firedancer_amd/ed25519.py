@@ -339,7 +339,7 @@ class Ed25519Gpu:
             self._keep.popleft()
         return r == GPU_OK
 
-    _HOST_STATS = ("scan_ns", "stage_ns", "h2d_ns", "launch_ns", "out_ns", "h2d_bytes")
+    _HOST_STATS = ("scan_ns", "stage_ns", "h2d_ns", "launch_ns", "out_ns", "h2d_bytes", "late_recs")
 
     def host_stats(self, reset=False):
         """fd_ed25519_gpu_host_stats: host time of the submit paths (ns) and the

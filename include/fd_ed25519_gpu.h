@@ -110,10 +110,12 @@ int                fd_ed25519_gpu_device_cnt( fd_ed25519_gpu_t const * ctx );
    records / rebased descriptors into page-locked staging, h2d = issuing the
    copies to HBM (a pageable source makes this a staged, synchronous copy),
    launch = kernel launches and events; out = codes / statuses copied to the
-   caller at poll; h2d_bytes = bytes sent.  reset != 0 zeroes them after
-   the read. */
+   caller at poll; h2d_bytes = bytes sent; late_recs = frag records the
+   poll found still unwritten after the batch's completion event and waited
+   for (0 unless the device's stores reach the host after the event).
+   reset != 0 zeroes them after the read. */
 typedef struct {
-  uint64_t scan_ns, stage_ns, h2d_ns, launch_ns, out_ns, h2d_bytes;
+  uint64_t scan_ns, stage_ns, h2d_ns, launch_ns, out_ns, h2d_bytes, late_recs;
 } fd_ed25519_gpu_host_stats_t;
 int                fd_ed25519_gpu_host_stats( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_host_stats_t * out, int reset );
 /* Metrics: verify kernel launches so far by kind (pipelined; one-shot,
