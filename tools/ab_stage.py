@@ -8,7 +8,12 @@ streaming rate per setting and checks every setting's results equal the
 first's.
 
   python3 tools/ab_stage.py "A:" "B:FD_ED25519_GPU_PARSE_STREAM=1" [--frags N] [--rounds R]
-  (a setting's BATCH=<frags> gives it its own batch size)
+  (a setting's BATCH=<frags> gives it its own batch size; HEAD=a/b/c its first
+  batches' sizes in frags, TAIL=x/y its last batches' sizes as fractions of
+  the batch -- bench_verify_stage.batch_schedule)
+  --per-run: each measurement is ONE pass from an idle stage, fill and drain
+  included (the stage bench's per-run figure), instead of --passes passes as
+  one stream
 """
 import argparse
 import os
@@ -30,6 +35,7 @@ ap.add_argument("--frags", type=int, default=1 << 20)
 ap.add_argument("--passes", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--batch", type=int, default=36000)
+ap.add_argument("--per-run", action="store_true")
 a = ap.parse_args()
 arena, frags, n_sigs = make_stream(a.frags, 0.1)
 fr = np.ascontiguousarray(frags)
@@ -39,6 +45,8 @@ for sp in a.settings:
     specs.append((name, dict(kv.split("=", 1) for kv in env.split(",")) if env else {}))
 # BATCH=<frags> in a setting: that setting's batch size (not an environment variable)
 bsz = [int(env.pop("BATCH", a.batch)) for _, env in specs]
+heads = [[int(x) for x in env.pop("HEAD").split("/")] if "HEAD" in env else [] for _, env in specs]
+tails = [[float(x) for x in env.pop("TAIL").split("/")] if "TAIL" in env else [] for _, env in specs]
 ctx = []
 for (name, env), b in zip(specs, bsz):
     saved = {k: os.environ.get(k) for k in env}
@@ -57,23 +65,27 @@ res = [np.zeros(len(fr), np.int8) for _ in specs]
 sig = np.zeros(len(fr), np.uint64)
 
 
-def stream(st, out, passes, batch):
+def stream(st, out, passes, k):
     st.tcache.reset()
-    return passes * n_sigs / stream_passes(st, arena, fr, out, sig, passes, batch)
+    return passes * n_sigs / stream_passes(st, arena, fr, out, sig, passes, bsz[k], heads[k], tails[k])
 
 
-for (g, st), out, b in zip(ctx, res, bsz):
-    stream(st, out, 1, b)                   # warm
+passes = 1 if a.per_run else a.passes
+for k, (g, st) in enumerate(ctx):
+    stream(st, res[k], 1, k)                # warm
 rates = [[] for _ in specs]
 for r in range(a.rounds):
     order = range(len(specs)) if r % 2 == 0 else reversed(range(len(specs)))
     for k in order:
-        rates[k].append(stream(ctx[k][1], res[k], a.passes, bsz[k]))
+        rates[k].append(stream(ctx[k][1], res[k], passes, k))
 for k, (name, env) in enumerate(specs):
     assert np.count_nonzero(res[k] != res[0]) <= 16, name
-    print("%-10s %-40s streaming median %.1f M sigs/s (min %.1f max %.1f)" % (
-        name, ",".join(["%s=%s" % kv for kv in env.items()] + ["batch=%d" % bsz[k]]), statistics.median(rates[k]) / 1e6,
-        min(rates[k]) / 1e6, max(rates[k]) / 1e6), flush=True)
+    print("%-10s %-50s %s median %.1f M sigs/s (mean %.1f, min %.1f max %.1f, %d runs)" % (
+        name, ",".join(["%s=%s" % kv for kv in env.items()] + ["batch=%d" % bsz[k]] +
+                       (["head=%s" % "/".join(map(str, heads[k]))] if heads[k] else []) +
+                       (["tail=%s" % "/".join(map(str, tails[k]))] if tails[k] else [])),
+        "per-run" if a.per_run else "streaming", statistics.median(rates[k]) / 1e6,
+        statistics.mean(rates[k]) / 1e6, min(rates[k]) / 1e6, max(rates[k]) / 1e6, len(rates[k])), flush=True)
 for i, (g, st) in enumerate(ctx):
     st.close()
     if i == 0:

@@ -42,7 +42,26 @@ def make_stream(n_frags, dup, seed=5):
     return arena, frags, sum(cnts[i] for i in order)
 
 
-def stream_passes(ast, arena, fr, res, sig, passes, batch):
+def batch_schedule(total, batch, head=(), tail=()):
+    """Batch sizes for a run of `total` frags from an idle stage: the `head`
+    sizes first (a ramp: the first launch starts after a short copy and the
+    link streams the next batches while the pipe fills), full `batch`es, then
+    the `tail` sizes (fractions of `batch`: short last batches make the drain
+    launches, which run one or two phases alone, short).  Sizes that do not
+    fit are dropped from the tail first, then the head."""
+    head = [int(h) for h in head if h > 0]
+    tail = [max(1, int(batch * f)) for f in tail]
+    while tail and sum(head) + sum(tail) > total:
+        tail.pop(0)
+    while head and sum(head) > total:
+        head.pop()
+    mid = total - sum(head) - sum(tail)
+    sizes = head + [batch] * (mid // batch) + ([mid % batch] if mid % batch else []) + tail
+    assert sum(sizes) == total and all(0 < z <= batch for z in sizes), (sizes, total, batch)
+    return sizes
+
+
+def stream_passes(ast, arena, fr, res, sig, passes, batch, head=(), tail=()):
     """`passes` passes over the frags fr as ONE stream into the async stage
     ast, like a tile that never stops: batches of `batch` frags cut
     continuously, so a batch may run from the end of one pass into the start
@@ -53,11 +72,12 @@ def stream_passes(ast, arena, fr, res, sig, passes, batch):
     import firedancer_amd as fa
     n = len(fr)
     total, k = passes * n, 0
+    sizes = batch_schedule(total, batch, head, tail)
     fifo = []
     t = time.perf_counter()
     while k < total or ast.pending():
         if k < total and ast.pending() < fa.STAGE_DEPTH:
-            i, m = k % n, min(batch, total - k)
+            i, m = k % n, sizes.pop(0)
             if i + m <= n:
                 ast.submit(arena, len(arena), fr[i:i + m], res[i:i + m], sig[i:i + m])
                 fifo.append(None)
