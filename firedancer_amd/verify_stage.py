@@ -132,11 +132,12 @@ class AsyncStage:
         self._keep = []
 
     def submit(self, arena, arena_sz, frags, result, sig):
-        """Enqueue a batch (arrays must stay alive until its poll returns 0)."""
+        """Enqueue a batch (arrays must stay alive until its poll returns 0).
+        Raises GpuError with ERR_BUSY when STAGE_DEPTH batches are outstanding
+        (poll the oldest first), like Ed25519Gpu.submit: a dropped batch must
+        never pass silently."""
         r = self.lib.fd_ed25519_gpu_stage_submit(self.st, _ptr(arena), arena_sz, _ptr(frags), len(frags),
                                                  _ptr(result), _ptr(sig))
-        if r == -104:
-            return False
         if r:
             raise GpuError("fd_ed25519_gpu_stage_submit: %s (%d)" % (strerror(r), r))
         self._keep.append((arena, frags, result, sig))

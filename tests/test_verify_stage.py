@@ -909,7 +909,9 @@ def test_stage_in_launch_parse_two_contexts_concurrently(ref):
     def run(g, batches, res, sig, errs):
         try:
             ast = fa.AsyncStage(g, fa.TCache(), 10000, threads=4, device_parse=True)
-            for b, r, s in zip(batches, res, sig):
+            for b, r, s in zip(batches, res, sig):          # nine batches: one more than STAGE_DEPTH
+                if ast.pending() == fa.STAGE_DEPTH:
+                    ast.poll(True)
                 ast.submit(arena_u, len(arena_u), np.ascontiguousarray(b), r, s)
             while ast.pending():
                 ast.poll(True)
