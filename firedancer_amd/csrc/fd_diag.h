@@ -17,6 +17,13 @@
      FD_DIAG_NT_INV=1|2|3    vector L1 / L2 / both invalidated at phase B/C start
      FD_DIAG_SC_INV_AFTER    L2 invalidated once phase B's tables are stored
      FD_DIAG_COMB_POS=k      only k comb additions
+     FD_DIAG_NO_HAND         pipe kernel: no hand-off, partial-sum or check-code traffic
+                             between the phases (phase A's stores folded into one
+                             never-taken store, phases B / C on synthetic inputs: the
+                             base point as A and R, hashed digit scalars)
+     FD_DIAG_NO_ARENA        pipe kernel: phase A reads no descriptor and no arena byte
+                             (synthetic descriptor, the base point as A and R, a small S,
+                             hashed message words)
      FD_DIAG_LSORT_TIMEOUT   every phase-A length-order wait expires
      FD_DIAG_PIPE_OVERLAP    (host) no cross-stream order on the table scratch */
 
@@ -27,7 +34,7 @@
 #if defined(FD_DIAG_NO_VTAB_STORE) || defined(FD_DIAG_VTAB_ONE_ENTRY) || defined(FD_DIAG_VTAB_NO_TAIL) || \
     defined(FD_DIAG_SC_TABLES) || defined(FD_DIAG_NT_TABLES) || defined(FD_DIAG_NT_INV) ||                 \
     defined(FD_DIAG_SC_INV_AFTER) || defined(FD_DIAG_COMB_POS) || defined(FD_DIAG_LSORT_TIMEOUT) ||         \
-    defined(FD_DIAG_PIPE_OVERLAP)
+    defined(FD_DIAG_PIPE_OVERLAP) || defined(FD_DIAG_NO_HAND) || defined(FD_DIAG_NO_ARENA)
 #error "FD_DIAG_* builds a wrong-results diagnostic variant: only tools/build_var.sh (FD_DIAG_BUILD) may define one"
 #endif
 #endif
@@ -42,6 +49,21 @@
 #define FD_DIAG_PHASE_BC_ENTRY()         do {} while( 0 )
 #define FD_DIAG_AFTER_TABLES()           do {} while( 0 )
 #define FD_DIAG_SCR_ORDER                1                 /* host: cross-stream wait on the scratch */
+#define FD_DIAG_NO_HAND_ON               0
+#define FD_DIAG_NO_ARENA_ON              0
+
+/* The synthetic inputs of the NO_HAND / NO_ARENA builds (only those builds
+   call these): word j of the base point's encoding (y = 4/5: bytes 0x58,
+   0x66 x 31), and a hashed word for slot g, word j (digits spread like a
+   real batch's, so the table fetches keep their distribution). */
+#if defined(__HIPCC__)
+__device__ __forceinline__ uint32_t fd_diag_bp_word( int j ) { return j ? 0x66666666u : 0x66666658u; }
+__device__ __forceinline__ uint32_t fd_diag_hash( uint64_t g, uint32_t j ) {
+  uint32_t x = (uint32_t)g * 0x9e3779b1u ^ (j + 1u) * 0x85ebca6bu;
+  x ^= x >> 15; x *= 0x2c1b3c6du; x ^= x >> 12; x *= 0x297a2d39u; x ^= x >> 15;
+  return x;
+}
+#endif
 
 #if defined(FD_DIAG_BUILD)
 
@@ -63,6 +85,16 @@
 #if defined(FD_DIAG_PIPE_OVERLAP)
 #undef  FD_DIAG_SCR_ORDER
 #define FD_DIAG_SCR_ORDER 0
+#endif
+
+#if defined(FD_DIAG_NO_HAND)
+#undef  FD_DIAG_NO_HAND_ON
+#define FD_DIAG_NO_HAND_ON 1
+#endif
+
+#if defined(FD_DIAG_NO_ARENA)
+#undef  FD_DIAG_NO_ARENA_ON
+#define FD_DIAG_NO_ARENA_ON 1
 #endif
 
 #if defined(FD_DIAG_VTAB_ONE_ENTRY)
