@@ -6,7 +6,7 @@
 #                                       or $FD_ED25519_GPU_LIB
 #   tools/gpu.sh ab A.so B.so ...       back-to-back A/B of library builds in one process
 #                                       (tools/ab_b2b.py, codes checked); $TAG names the log
-#   tools/gpu.sh bytes A.so B.so ...    per build: FETCH_SIZE, WRITE_SIZE and GRBM/SQ passes over
+#   tools/gpu.sh bytes A.so B.so ...    per build: FETCH_SIZE, WRITE_SIZE, read requests by size and GRBM/SQ passes over
 #                                       steady-state pipe launches -> gpurun_out/bytes_$TAG.jsonl
 #   tools/gpu.sh bench [bench args]     one bench.py line -> gpurun_out/bench_$TAG.json
 #   tools/gpu.sh profile [bench args]   bench lines, kernel trace + PMC set of bench.py -> gpurun_out/prof_$TAG/
@@ -42,7 +42,8 @@ case "$cmd" in
     : > gpurun_out/bytes_$T.jsonl
     for L in "$@"; do
       b=$(basename $L .so); o=gpurun_out/bytes_$T/$b; mkdir -p $o
-      for pass in "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
+      for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B" \
+                  "GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
         p=${pass%% *}
         AB_ROUNDS=2 timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d $o/$p -o pmc -- \
           python3 tools/ab_b2b.py $L 20 > $o/$p.out 2> $o/$p.err

@@ -38,6 +38,15 @@ for path in a.csv:
 if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
     out["hbm_bytes_per_launch"] = (2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024
     out["hbm_bytes_per_verify"] = out["hbm_bytes_per_launch"] / a.n
+if "TCC_EA0_RDREQ_128B" in out:
+    # the fabric read requests by size (TCC_EA0_RDREQ_{32B,64B,128B}): the read bytes counted exactly,
+    # whatever the access width (FETCH_SIZE on gfx950 tallies every non-32-B request at 64 B, so the
+    # guide's x2 is exact only for 128-B requests)
+    n32, n64, n128 = out["TCC_EA0_RDREQ_32B"], out["TCC_EA0_RDREQ_64B"], out["TCC_EA0_RDREQ_128B"]
+    out["read_bytes_by_request_size"] = 32 * n32 + 64 * n64 + 128 * n128
+    out["read_requests_accounted"] = (n32 + n64 + n128) / out["TCC_EA0_RDREQ"] if out.get("TCC_EA0_RDREQ") else None
+    if "WRITE_SIZE" in out:
+        out["hbm_bytes_per_verify_by_request_size"] = (out["read_bytes_by_request_size"] + out["WRITE_SIZE"] * 1024) / a.n
 if "GRBM_GUI_ACTIVE" in out:
     out["clock_ghz"] = out["GRBM_GUI_ACTIVE"] / 8 / out["dur_ms_median"] / 1e6
 print(json.dumps(out))
