@@ -62,21 +62,6 @@
 #ifndef FD_OPT_APARSE
 #define FD_OPT_APARSE 1
 #endif
-/*   TOUCH     (round 6) arena reads.  A lane reads its signature, its key and
-               each SHA block's message window as dwords (alignbyte for any
-               byte offset): 9-33 loads to the same one or two 128-B lines,
-               issued back to back.  Issued before the first had returned,
-               each one missed L2 and became a fabric read of the whole line:
-               4.2 KB of HBM reads per verify for the 312 B of descriptor,
-               signature, key and message (the round-6 byte ledger, the
-               NO_ARENA build's difference).  With TOUCH one dword per line
-               goes first and the window's loads are issued once it has come
-               back: the signature's, key's and block 0's lines in one wait
-               before phase A's loads, block b+1's lines before block b's
-               compression and its 33 loads after it. */
-#ifndef FD_OPT_TOUCH
-#define FD_OPT_TOUCH 1
-#endif
 
 /* Diagnostic build only (-DFD_PHASE_STAMPS, tools/Makefile): s_memtime at
    phase boundaries, per-wave deltas summed into args.stamps.  The product
@@ -105,18 +90,6 @@ __device__ __forceinline__ void load_words( uint32_t out[ N ], uint8_t const * a
     out[i] = __builtin_amdgcn_alignbyte( nxt, prev, sh );
     prev = nxt;
   }
-}
-
-/* Consume a loaded value without using it: the compiler waits for the load
-   here (s_waitcnt) and moves no memory access across (the "memory"
-   clobber). */
-__device__ __forceinline__ void fd_consume( uint32_t x ) { asm volatile( "" :: "v"(x) : "memory" ); }
-
-/* One dword of each 128-B line under bytes [off, off + n), n <= 128: the
-   first and the last byte's dwords (clamped like load_words), XORed (a value
-   to consume; the loads only bring the lines into L2). */
-__device__ __forceinline__ uint32_t arena_touch( uint32_t const * a32, uint32_t off, uint32_t n, uint32_t lim_dw ) {
-  return a32[ min( off >> 2, lim_dw ) ] ^ a32[ min( (off + n - 1u) >> 2, lim_dw ) ];
 }
 
 /* ------------------------------------------------------------------ B tables */
@@ -198,18 +171,9 @@ __device__ __forceinline__ void sha_fetch( uint32_t raw[ 33 ], uint32_t const * 
 #endif
 }
 
-/* The two lines of block b's raw window (sha_fetch's dwords start .. start +
-   32, clamped the same way), one dword each. */
-__device__ __forceinline__ uint32_t sha_touch( uint32_t const * a32, uint32_t msg_off, uint32_t b, uint32_t lim_dw ) {
-  int32_t start = (int32_t)(msg_off >> 2) + 32*(int32_t)b - 16;
-  return a32[ min( (uint32_t)max( start, 0 ), lim_dw ) ] ^ a32[ min( (uint32_t)max( start + 32, 0 ), lim_dw ) ];
-}
-
 /* SHA-512(R || A || M) mod l.  R, A: 8 LE words each; the message is
-   streamed from HBM: FD_OPT_TOUCH (the caller touched block 0's lines with
-   the signature's) touches block b+1's two lines before block b's
-   compression and loads its window after it; otherwise each block's dwords
-   are fetched one block ahead. */
+   streamed from HBM, each block's dwords fetched one block ahead so the
+   load latency hides behind the previous compression. */
 template<bool FASTBLK>
 __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 ], uint32_t const Aw[ 8 ],
                                           uint8_t const * arena, uint32_t msg_off, uint32_t msg_sz, uint32_t lim_dw ) {
@@ -224,12 +188,7 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
     uint32_t raw[ 33 ];
 #pragma unroll
     for( int i=0; i<33; i++ ) raw[i] = nxt[i];
-#if FD_OPT_TOUCH
-    uint32_t tch = b + 1u < nblk ? sha_touch( a32, msg_off, b + 1u, lim_dw ) : 0u;
-    FE_FENCE();
-#else
     if( b + 1u < nblk ) sha_fetch( nxt, a32, msg_off, b + 1u, lim_dw );
-#endif
     uint64_t W[ 16 ];
     /* a block whose message bytes all lie before msg_sz on every lane of
        the wave (every block but the last one or two) needs no padding
@@ -278,9 +237,6 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
     }
     }
     sha512_compress( h, W );
-#if FD_OPT_TOUCH
-    if( b + 1u < nblk ) { fd_consume( tch ); sha_fetch( nxt, a32, msg_off, b + 1u, lim_dw ); }
-#endif
   }
   uint32_t dg[ 16 ];
 #pragma unroll
@@ -996,11 +952,6 @@ fd_ed25519_verify_kernel( verify_args args ) {
 #pragma unroll
   for( int j=0; j<8; j++ ) pub[j] = 0u;
   if( desc_ok ) {
-#if FD_OPT_TOUCH
-    fd_consume( arena_touch( (uint32_t const *)args.arena, d.sig_off, 64u, lim_dw ) ^
-                arena_touch( (uint32_t const *)args.arena, d.pub_off, 32u, lim_dw ) ^
-                sha_touch( (uint32_t const *)args.arena, d.msg_off, 0u, lim_dw ) );
-#endif
     load_words<16>( sig, args.arena, d.sig_off, lim_dw );
     load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
   }
@@ -1151,11 +1102,6 @@ fd_ed25519_verify_pair_kernel( verify_args args ) {
 #pragma unroll
   for( int j=0; j<8; j++ ) pub[j] = 0u;
   if( desc_ok ) {
-#if FD_OPT_TOUCH
-    fd_consume( arena_touch( (uint32_t const *)args.arena, d.sig_off, 64u, lim_dw ) ^
-                arena_touch( (uint32_t const *)args.arena, d.pub_off, 32u, lim_dw ) ^
-                sha_touch( (uint32_t const *)args.arena, d.msg_off, 0u, lim_dw ) );
-#endif
     load_words<16>( sig, args.arena, d.sig_off, lim_dw );
     if( !role ) load_words<8>( pub, args.arena, d.pub_off, lim_dw );
   }
@@ -1412,11 +1358,6 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #pragma unroll
       for( int j=0; j<8; j++ ) sig[8+j] = j < 7 ? fd_diag_hash( gid, 100u + (uint32_t)j ) : 0x0fffffffu & fd_diag_hash( gid, 107u );
 #else
-#if FD_OPT_TOUCH
-      uint32_t const * a32 = (uint32_t const *)args.arena;
-      fd_consume( arena_touch( a32, d.sig_off, 64u, lim_dw ) ^ arena_touch( a32, d.pub_off, 32u, lim_dw ) ^
-                  sha_touch( a32, d.msg_off, 0u, lim_dw ) );
-#endif
       load_words<16>( sig, args.arena, d.sig_off, lim_dw );
       load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
 #endif
@@ -1966,11 +1907,6 @@ fd_ed25519_verify_cached_kernel( verify_args args ) {
 #pragma unroll
   for( int j=0; j<8; j++ ) pub[j] = 0u;
   if( desc_ok ) {
-#if FD_OPT_TOUCH
-    fd_consume( arena_touch( (uint32_t const *)args.arena, d.sig_off, 64u, lim_dw ) ^
-                arena_touch( (uint32_t const *)args.arena, d.pub_off, 32u, lim_dw ) ^
-                sha_touch( (uint32_t const *)args.arena, d.msg_off, 0u, lim_dw ) );
-#endif
     load_words<16>( sig, args.arena, d.sig_off, lim_dw );
     load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
   }
