@@ -8,6 +8,7 @@
 #                                       (tools/ab_b2b.py, codes checked); $TAG names the log
 #   tools/gpu.sh bytes A.so B.so ...    per build: FETCH_SIZE, WRITE_SIZE, read requests by size and GRBM/SQ passes over
 #                                       steady-state pipe launches -> gpurun_out/bytes_$TAG.jsonl
+#   tools/gpu.sh phasebytes [--reps N]  each pipe phase's bytes alone (tools/phase_bytes.py) -> gpurun_out/phasebytes_$TAG.json
 #   tools/gpu.sh bench [bench args]     one bench.py line -> gpurun_out/bench_$TAG.json
 #   tools/gpu.sh profile [bench args]   bench lines, kernel trace + PMC set of bench.py -> gpurun_out/prof_$TAG/
 #                                       (then tools/summarize_profile.py gpurun_out/prof_$TAG profiles/rNN)
@@ -50,6 +51,16 @@ case "$cmd" in
       done
       python3 tools/pmc_med.py --tag $b $o/*/pmc_counter_collection.csv | tee -a gpurun_out/bytes_$T.jsonl
     done ;;
+  phasebytes)
+    # each pipe phase alone (tools/phase_bytes.py): FETCH, WRITE and read-request-size passes
+    cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+    o=gpurun_out/phasebytes_$T; mkdir -p $o
+    for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B"; do
+      p=${pass%% *}
+      timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d $o/$p -o pmc -- python3 tools/phase_bytes.py "$@" \
+        > $o/$p.out 2> $o/$p.err
+    done
+    python3 tools/phase_bytes.py --summarize $o/*/pmc_counter_collection.csv | tee gpurun_out/phasebytes_$T.json ;;
   bench)
     timeout -k 10 300 python3 bench.py "$@" > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err \
       || { tail -20 gpurun_out/bench_$T.err; exit 1; }
