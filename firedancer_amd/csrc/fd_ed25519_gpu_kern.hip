@@ -62,6 +62,20 @@
 #ifndef FD_OPT_APARSE
 #define FD_OPT_APARSE 1
 #endif
+/*   APRIO     (round 6) the pipe kernel's phase-A waves are the youngest on
+               their SIMD, so the arbiter (oldest first) gives them the issue
+               slots phases C and B leave: a SHA block's 33 dword loads (and
+               the signature's and key's 26) came out spread over many
+               microseconds, and the L2 -- streaming ~4 MB of table reads per
+               XCD every ~15 us -- had dropped a window's two lines before the
+               window's last loads reached them: 4.2 KB of HBM reads per
+               verify for 312 B in the steady state, 322 B with phase A alone
+               (tools/phase_bytes.py).  APRIO issues each window's loads at
+               the top wave priority (s_setprio 3 around them, back to 0
+               after), so they leave within a few hundred cycles. */
+#ifndef FD_OPT_APRIO
+#define FD_OPT_APRIO 1
+#endif
 
 /* Diagnostic build only (-DFD_PHASE_STAMPS, tools/Makefile): s_memtime at
    phase boundaries, per-wave deltas summed into args.stamps.  The product
@@ -182,13 +196,19 @@ __device__ __forceinline__ void hash_ram( uint32_t k[ 8 ], uint32_t const Rw[ 8 
   uint32_t nblk = (total + 17u + 127u) >> 7;
   uint32_t const * a32 = (uint32_t const *)arena;
   uint32_t sh = msg_off & 3u;
+  /* the <false> instantiation is the pipe kernel's phase A (FD_OPT_APRIO) */
+  constexpr bool APRIO = !FASTBLK && FD_OPT_APRIO;
   uint32_t nxt[ 33 ];
+  if( APRIO ) { FE_FENCE(); __builtin_amdgcn_s_setprio( 3 ); FE_FENCE(); }
   sha_fetch( nxt, a32, msg_off, 0u, lim_dw );
+  if( APRIO ) { FE_FENCE(); __builtin_amdgcn_s_setprio( 0 ); FE_FENCE(); }
   for( uint32_t b=0; b<nblk; b++ ) {
     uint32_t raw[ 33 ];
 #pragma unroll
     for( int i=0; i<33; i++ ) raw[i] = nxt[i];
+    if( APRIO ) { FE_FENCE(); __builtin_amdgcn_s_setprio( 3 ); FE_FENCE(); }
     if( b + 1u < nblk ) sha_fetch( nxt, a32, msg_off, b + 1u, lim_dw );
+    if( APRIO ) { FE_FENCE(); __builtin_amdgcn_s_setprio( 0 ); FE_FENCE(); }
     uint64_t W[ 16 ];
     /* a block whose message bytes all lie before msg_sz on every lane of
        the wave (every block but the last one or two) needs no padding
@@ -1358,8 +1378,14 @@ fd_ed25519_verify_pipe_kernel( pipe_args a ) {
 #pragma unroll
       for( int j=0; j<8; j++ ) sig[8+j] = j < 7 ? fd_diag_hash( gid, 100u + (uint32_t)j ) : 0x0fffffffu & fd_diag_hash( gid, 107u );
 #else
+#if FD_OPT_APRIO
+      FE_FENCE(); __builtin_amdgcn_s_setprio( 3 ); FE_FENCE();
+#endif
       load_words<16>( sig, args.arena, d.sig_off, lim_dw );
       load_words<8> ( pub, args.arena, d.pub_off, lim_dw );
+#if FD_OPT_APRIO
+      FE_FENCE(); __builtin_amdgcn_s_setprio( 0 ); FE_FENCE();
+#endif
 #endif
     }
     bool bad_s = desc_ok && !sc_lt_l( sig + 8 );                         /* :157-159 */
