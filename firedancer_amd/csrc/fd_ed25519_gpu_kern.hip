@@ -76,6 +76,16 @@
 #ifndef FD_OPT_APRIO
 #define FD_OPT_APRIO 1
 #endif
+/*   X4        (round 6) the arena windows (a SHA block's 33 dwords, the
+               signature's 17, the key's 9) as 16-byte loads from their
+               dword-aligned start (gfx950 takes a dwordx4 at any 4-byte
+               alignment) at immediate offsets from one base: 9 / 5 / 3 load
+               instructions and no per-dword address arithmetic, when the
+               whole window lies inside the readable arena for every lane of
+               the wave (else the clamped dword loads). */
+#ifndef FD_OPT_X4
+#define FD_OPT_X4 1
+#endif
 
 /* Diagnostic build only (-DFD_PHASE_STAMPS, tools/Makefile): s_memtime at
    phase boundaries, per-wave deltas summed into args.stamps.  The product
@@ -93,10 +103,38 @@
 
 /* n little-endian words starting at an arbitrary byte offset off (read
    through aligned dwords, clamped to the readable arena). */
+typedef unsigned int fd_u4a4 __attribute__(( ext_vector_type( 4 ), aligned( 4 ) ));   /* 16-byte load, 4-byte alignment */
+
+/* raw[0 .. M) = a32[dw .. dw + M) (M = 4 k + 1) as k dwordx4 + 1 dword
+   from one base address (FD_OPT_X4's fast path; the caller checked the
+   range) */
+template<int M>
+__device__ __forceinline__ void load_x4( uint32_t raw[ M ], uint32_t const * a32, uint32_t dw ) {
+  static_assert( (M & 3) == 1, "M = 4 k + 1" );
+  uint32_t const * p = a32 + dw;
+#pragma unroll
+  for( int j=0; j<M/4; j++ ) {
+    fd_u4a4 v = *(fd_u4a4 const *)(p + 4*j);
+    raw[4*j] = v.x; raw[4*j+1] = v.y; raw[4*j+2] = v.z; raw[4*j+3] = v.w;
+  }
+  raw[M-1] = p[M-1];
+}
+
 template<int N>
 __device__ __forceinline__ void load_words( uint32_t out[ N ], uint8_t const * arena, uint32_t off, uint32_t lim_dw ) {
   uint32_t const * a32 = (uint32_t const *)arena;
   uint32_t dw = off >> 2, sh = off & 3u;
+#if FD_OPT_X4
+  if constexpr( (N & 3) == 0 ) {
+    if( __all( dw + (uint32_t)N <= lim_dw ) ) {
+      uint32_t raw[ N + 1 ];
+      load_x4<N + 1>( raw, a32, dw );
+#pragma unroll
+      for( int i=0; i<N; i++ ) out[i] = __builtin_amdgcn_alignbyte( raw[i+1], raw[i], sh );
+      return;
+    }
+  }
+#endif
   uint32_t prev = a32[ min( dw, lim_dw ) ];
 #pragma unroll
   for( int i=0; i<N; i++ ) {
@@ -180,6 +218,9 @@ __device__ __forceinline__ void sha_fetch( uint32_t raw[ 33 ], uint32_t const * 
 #pragma unroll
   for( int i=0; i<33; i++ ) raw[i] = fd_diag_hash( (uint64_t)msg_off, (uint32_t)(start + i) );
 #else
+#if FD_OPT_X4
+  if( __all( start >= 0 && (uint32_t)start + 32u <= lim_dw ) ) { load_x4<33>( raw, a32, (uint32_t)start ); return; }
+#endif
 #pragma unroll
   for( int i=0; i<33; i++ ) raw[i] = a32[ min( (uint32_t)max( start + i, 0 ), lim_dw ) ];
 #endif
