@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench_offload.py -- the verify tile's side of the GPU offload link
 (include/fd_verify_offload.h), measured end to end
-across two processes.  Run tools/offload_e2e.sh, which starts
+across two processes.  Run `tools/gpu.sh offload`, which starts
 firedancer_amd/fd_verify_offload_server (the process that owns the GPU)
 and then this client, which never touches the GPU -- like the sandboxed
 tile: it publishes --frags synthetic signed transactions (tools/synth.py,

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""summarize_profile.py -- turn a tools/profile.sh output directory
+"""summarize_profile.py -- turn a `tools/gpu.sh profile` output directory
 (gpurun_out/prof_<tag>) into the committed summaries under profiles/<tag>/:
 
   kernel_stats.csv    rocprofv3 --kernel-trace --stats summary (verbatim)
