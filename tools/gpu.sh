@@ -55,7 +55,8 @@ case "$cmd" in
     # each pipe phase alone (tools/phase_bytes.py): FETCH, WRITE and read-request-size passes
     cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
     o=gpurun_out/phasebytes_$T; mkdir -p $o
-    for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B"; do
+    for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B" \
+                "SQ_INSTS_VALU SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
       p=${pass%% *}
       timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d $o/$p -o pmc -- python3 tools/phase_bytes.py "$@" \
         > $o/$p.out 2> $o/$p.err

@@ -54,6 +54,9 @@ if a.summarize:
                                                           128 * o["TCC_EA0_RDREQ_128B"]) / a.n
         if "WRITE_SIZE" in o:
             o["write_bytes_per_verify"] = o["WRITE_SIZE"] * 1024 / a.n
+        if "SQ_INSTS_VALU" in o:
+            # one wave per 64 signatures runs the phase: VALU wave-instructions per 64 signatures
+            o["valu_per_64_sigs"] = o["SQ_INSTS_VALU"] / (a.n / 64)
     print(json.dumps(out, indent=1))
     sys.exit(0)
 
