@@ -44,6 +44,14 @@
 
 #define FD_LAT_MAX_ITER 1024
 
+/* FD_OPT_LATSTEP: the Lehmer step with a low-biased reciprocal (one
+   quotient correction instead of two, one Newton step instead of two) and
+   the exactness tests on S = q EB + EA (48 instead of 61 VALU a step).  It
+   leaves every lane's remainder sequence, hence (u, v), unchanged. */
+#ifndef FD_OPT_LATSTEP
+#define FD_OPT_LATSTEP 1
+#endif
+
 /* 8l as 8 LE words */
 #define FD_N8L0 0xe7ae9f68u
 #define FD_N8L1 0xc09318d2u
@@ -177,6 +185,24 @@ FD_LT_FN double lat_rcp( double y ) {
 #endif
 }
 
+/* 1/y rounded DOWN by ~2^-35 relative: the hardware reciprocal, relative
+   error e (at most 2^-24.36 over 2^32 mantissas, tools/rcp_probe.hip,
+   profiles/r06/rcp_probe.json; the argument needs e < 2^-18), and one
+   Newton step whose constant carries the bias: r (2 - 2^-35 - y r) =
+   (1/y)(1 - e^2 - 2^-35 (1 + e)), an underestimate by 2^-35 (1 -+ 2^-17)
+   at most 2^-34.4.  A quotient q* below 2^27 is then floor(A
+   lat_rcp_lo(B)) or one more (A lat_rcp_lo(B) > q* - 1 and, after the
+   product's 2^-53 rounding, still below A/B). */
+FD_LT_FN double lat_rcp_lo( double y ) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp( y );
+  return r * fma( -y, r, 2.0 - 0x1p-35 );
+#else
+  return (1.0 / y) * (1.0 - 0x1p-35);
+#endif
+}
+
+
 /* a < b, 8 words */
 FD_LT_FN int lat_lt( uint32_t const a[ 8 ], uint32_t const b[ 8 ] ) { return !lat_ge( a, b ); }
 
@@ -239,6 +265,21 @@ FD_LT_FN int lat_lehmer( uint32_t x[ 8 ], uint32_t tx[ 4 ], uint32_t y[ 8 ], uin
      every loop-carried double live in two register copies, ~20 moves a
      step; a lane that stopped computes on with its state held */
   while( lat_any( go ) ) {
+#if FD_OPT_LATSTEP
+    /* q from the low-biased reciprocal is the quotient or one less (a q
+       that is off by more is >= 2^26 and fails the matrix bound below) */
+    double q = floor( A * lat_rcp_lo( B ) );
+    double R = fma( -q, B, A );
+    int hi = R >= B;
+    q = hi ? q + 1.0 : q; R = hi ? R - B : R;
+    double EA = a0 + a1, EB = b0 + b1;
+    double nb0 = fma( q, b0, a0 ), nb1 = fma( q, b1, a1 );
+    /* S = nb0 + nb1 = q EB + EA; the tests below are the ones of the
+       form without FD_OPT_LATSTEP rewritten with S, exact whenever S <
+       2^26 (every operand is then an integer below 2^53) */
+    double S = fma( q, EB, EA );
+    int ok = go & (R >= S) & (B - R - EB > S) & (S < 67108864.0);
+#else
     double q = floor( A * lat_rcp( B ) );
     double R = fma( -q, B, A );
     int lo = R < 0.0;
@@ -247,15 +288,17 @@ FD_LT_FN int lat_lehmer( uint32_t x[ 8 ], uint32_t tx[ 4 ], uint32_t y[ 8 ], uin
     q = hi ? q + 1.0 : q; R = hi ? R - B : R;
     double EA = a0 + a1, EB = b0 + b1;
     double nb0 = fma( q, b0, a0 ), nb1 = fma( q, b1, a1 );
+    double S = nb0 + nb1;
     /* exact iff q <= true quotient < q+1 for every x/2^e0, y/2^e0 in
        their truncation intervals; keep every quantity below 2^53 */
-    int ok = go & (R - EA - q*EB >= 0.0) & (B - R - EA - (q + 1.0)*EB > 0.0) & (nb0 + nb1 < 67108864.0);
+    int ok = go & (R - EA - q*EB >= 0.0) & (B - R - EA - (q + 1.0)*EB > 0.0) & (S < 67108864.0);
+#endif
     A  = ok ? B   : A;  B  = ok ? R   : B;
     a0 = ok ? b0  : a0; a1 = ok ? b1  : a1;
     b0 = ok ? nb0 : b0; b1 = ok ? nb1 : b1;
     j += ok;
     /* stop once the new remainder might be < 2^128 (or shrank too far to steer) */
-    go = ok & (R - (nb0 + nb1) >= thr) & (R >= 67108864.0);
+    go = ok & (R - S >= thr) & (R >= 67108864.0);
   }
   if( act && j ) {
     /* (x', y') = j even: (a0 x - a1 y, b1 y - b0 x); j odd: negated */

@@ -198,8 +198,26 @@ def test_lattice_short_vector_host(lib):
         uu = val32(u) * (-1 if un.value else 1)
         vv = val32(v)
         assert vv % 2 == 1 and 0 < vv < LL and (uu - vv * k) % n8 == 0, (k, uu, vv)
+        if k and k % LL:
+            assert lat_euclid_check(k, uu, vv, n8), (k, uu, vv)
         bits.append(max(abs(uu).bit_length(), vv.bit_length()))
     assert max(bits[:20000]) <= 140 and sorted(bits[:20000])[19800] <= 131
+
+
+def lat_euclid_check(k, u, v, n8):
+    """The search's output is the one the exact extended Euclid on (8l, k)
+    gives: at the first remainder r_i < 2^128, (u, v) = (r_i, t_i) up to sign
+    when t_i is odd, else (r_{i-1} - j r_i, t_{i-1} - j t_i) for some j >= 0
+    (fd_lattice_dev.h).  Pins every quotient of the Lehmer rounds, not only
+    the lattice relation."""
+    r0, t0, r1, t1 = n8, 0, k, 1
+    while r1 >= 2**128:
+        q = r0 // r1
+        r0, r1, t0, t1 = r1, r0 - q * r1, t1, t0 - q * t1
+    if t1 % 2:
+        return (u, v) == ((r1, t1) if t1 > 0 else (-r1, -t1))
+    j, rem = divmod(v - abs(t0), abs(t1))
+    return rem == 0 and j >= 0 and u == (r0 - j * r1) * (1 if t0 > 0 else -1)
 
 
 def val32(w):

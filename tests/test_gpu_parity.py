@@ -162,6 +162,22 @@ def _words_to_int(w):
     return sum(int(x) << (32 * i) for i, x in enumerate(w))
 
 
+def lat_euclid_check(k, u, v, n8):
+    """The search's output is the one the exact extended Euclid on (8l, k)
+    gives: at the first remainder r_i < 2^128, (u, v) = (r_i, t_i) up to sign
+    when t_i is odd, else (r_{i-1} - j r_i, t_{i-1} - j t_i) for some j >= 0
+    (fd_lattice_dev.h).  Pins every quotient of the Lehmer rounds, not only
+    the lattice relation."""
+    r0, t0, r1, t1 = n8, 0, k, 1
+    while r1 >= 2**128:
+        q = r0 // r1
+        r0, r1, t0, t1 = r1, r0 - q * r1, t1, t0 - q * t1
+    if t1 % 2:
+        return (u, v) == ((r1, t1) if t1 > 0 else (-r1, -t1))
+    j, rem = divmod(v - abs(t0), abs(t1))
+    return rem == 0 and j >= 0 and u == (r0 - j * r1) * (1 if t0 > 0 else -1)
+
+
 def test_lattice_device_random_and_adversarial_k(gpu):
     """The device short-vector search (fd_lattice_dev.h) on 200K random k and
     structured k: u = v k (mod 8l), v odd, 0 < v < l -- the conditions that make
@@ -181,6 +197,8 @@ def test_lattice_device_random_and_adversarial_k(gpu):
         v = _words_to_int(out[i, 8:16])
         assert v % 2 == 1 and 0 < v < L_ORDER, (k, u, v)
         assert (u - v * k) % n8 == 0, (k, u, v)
+        if (i < 50_000 or i >= n) and k:
+            assert lat_euclid_check(k, u, v, n8), (k, u, v)
         bits.append(max(abs(u).bit_length(), v.bit_length()))
     # random k: the vectors are ~2^128 (what the ~130-doubling loop is sized for)
     assert max(bits[:n]) <= 140 and int(np.percentile(bits[:n], 99)) <= 131
