@@ -12,6 +12,9 @@
      FD_DIAG_NO_VTAB_STORE   table stores skipped, the math kept
      FD_DIAG_VTAB_ONE_ENTRY  every chain fetch reads row 0
      FD_DIAG_VTAB_NO_TAIL    the entries' 32-B tails never stored nor read
+     FD_DIAG_STORE_COAL      table stores coalesced per instruction (same bytes, wrong layout)
+     FD_DIAG_STORE_COAL_NT   the same, nontemporal
+     FD_DIAG_STORE_SMALL     table stores into one small region (no HBM writes)
      FD_DIAG_SC_TABLES       table stores at system scope (sc0 sc1)
      FD_DIAG_NT_TABLES       table stores nontemporal (correct, slower)
      FD_DIAG_NT_INV=1|2|3    vector L1 / L2 / both invalidated at phase B/C start
@@ -34,7 +37,8 @@
 #if defined(FD_DIAG_NO_VTAB_STORE) || defined(FD_DIAG_VTAB_ONE_ENTRY) || defined(FD_DIAG_VTAB_NO_TAIL) || \
     defined(FD_DIAG_SC_TABLES) || defined(FD_DIAG_NT_TABLES) || defined(FD_DIAG_NT_INV) ||                 \
     defined(FD_DIAG_SC_INV_AFTER) || defined(FD_DIAG_COMB_POS) || defined(FD_DIAG_LSORT_TIMEOUT) ||         \
-    defined(FD_DIAG_PIPE_OVERLAP) || defined(FD_DIAG_NO_HAND) || defined(FD_DIAG_NO_ARENA)
+    defined(FD_DIAG_PIPE_OVERLAP) || defined(FD_DIAG_NO_HAND) || defined(FD_DIAG_NO_ARENA) || defined(FD_DIAG_STORE_COAL) || \
+    defined(FD_DIAG_STORE_SMALL) || defined(FD_DIAG_STORE_COAL_NT)
 #error "FD_DIAG_* builds a wrong-results diagnostic variant: only tools/build_var.sh (FD_DIAG_BUILD) may define one"
 #endif
 #endif
@@ -106,6 +110,42 @@ __device__ __forceinline__ uint32_t fd_diag_hash( uint64_t g, uint32_t j ) {
 #undef  FD_DIAG_VTAB_STORE
 #define FD_DIAG_VTAB_STORE( m, tl, w ) do {                                                       \
     if( (w)[0] == 0xdeadbeefu && (w)[1] == 0xdeadbeefu ) (m)[0] = make_uint4( (w)[2], (w)[3], (w)[4], (w)[5] ); \
+    return; } while( 0 )
+#elif defined(FD_DIAG_STORE_COAL)
+/* the same bytes into the same 8 KB (main) / 2 KB (tail) region of the wave,
+   but chunk j of lane l at region + 1 KB j + 16 B l: every store instruction
+   one contiguous KB (8 whole lines) instead of 16 B in each of 64 lines
+   (wrong layout, so wrong codes: what the store pattern costs) */
+#undef  FD_DIAG_VTAB_STORE
+#define FD_DIAG_VTAB_STORE( m, tl, w ) do {                                                       \
+    uint32_t _l = threadIdx.x & 63u;                                                              \
+    uint4 * _m0 = (m) - 8u*_l; uint4 * _t0 = (tl) - 2u*_l;                                        \
+    for( int j=0; j<8; j++ ) _m0[ 64*j + _l ] = make_uint4( (w)[4*j], (w)[4*j+1], (w)[4*j+2], (w)[4*j+3] ); \
+    if( tail ) for( int j=0; j<2; j++ ) _t0[ 64*j + _l ] = make_uint4( (w)[32+4*j], (w)[33+4*j], (w)[34+4*j], (w)[35+4*j] ); \
+    return; } while( 0 )
+#elif defined(FD_DIAG_STORE_COAL_NT)
+/* FD_DIAG_STORE_COAL's pattern (8 whole lines per store instruction) as
+   nontemporal stores: the table bytes leave without taking L2 space */
+#undef  FD_DIAG_VTAB_STORE
+#define FD_DIAG_VTAB_STORE( m, tl, w ) do {                                                       \
+    typedef unsigned int u32x4 __attribute__(( ext_vector_type( 4 ) ));                           \
+    uint32_t _l = threadIdx.x & 63u;                                                              \
+    u32x4 * _m0 = (u32x4 *)((m) - 8u*_l); u32x4 * _t0 = (u32x4 *)((tl) - 2u*_l);                  \
+    for( int j=0; j<8; j++ ) { u32x4 v = { (w)[4*j], (w)[4*j+1], (w)[4*j+2], (w)[4*j+3] };        \
+      __builtin_nontemporal_store( v, _m0 + 64*j + _l ); }                                        \
+    if( tail ) for( int j=0; j<2; j++ ) { u32x4 v = { (w)[32+4*j], (w)[33+4*j], (w)[34+4*j], (w)[35+4*j] }; \
+      __builtin_nontemporal_store( v, _t0 + 64*j + _l ); }                                        \
+    return; } while( 0 )
+#elif defined(FD_DIAG_STORE_SMALL)
+/* the same store instructions (each lane its own 128-B / 32-B record), into
+   one 10 KB region per table side instead of the tables: no HBM write
+   traffic and no L2 capacity taken (wrong codes by design) */
+#undef  FD_DIAG_VTAB_STORE
+#define FD_DIAG_VTAB_STORE( m, tl, w ) do {                                                       \
+    uint32_t _l = threadIdx.x & 63u;                                                              \
+    uint4 * _m0 = (uint4 *)vtab + 8u*_l;         /* the first 10 KB of the table scratch */         \
+    for( int j=0; j<8; j++ ) _m0[ j ] = make_uint4( (w)[4*j], (w)[4*j+1], (w)[4*j+2], (w)[4*j+3] ); \
+    if( tail ) for( int j=0; j<2; j++ ) _m0[ 512 + 2*_l + j ] = make_uint4( (w)[32+4*j], (w)[33+4*j], (w)[34+4*j], (w)[35+4*j] ); \
     return; } while( 0 )
 #elif defined(FD_DIAG_SC_TABLES)
 #undef  FD_DIAG_VTAB_STORE
