@@ -421,8 +421,12 @@ struct fd_ed25519_gpu_stage {
   int                       threads;
   int                       devparse;      /* parse frags on the GPU when the context has room */
   int                       autoreg;       /* page-lock callers' frag areas (opt-in: FD_ED25519_GPU_STAGE_AUTOREG=1) */
-  int                       kick;          /* early drain launches when nothing waits: 1 the oldest batch's (default),
-                                              2 the newest's, 0 none (FD_ED25519_GPU_STAGE_KICK, A/Bs) */
+  int                       kick;          /* early drain launches when nothing waits: 1 the oldest batch's, the
+                                              newest's while the caller is blocked in stage_poll (default), 3 the
+                                              oldest's only, 2 the newest's, 0 none (FD_ED25519_GPU_STAGE_KICK, A/Bs) */
+  int                       poll_blocked;  /* callers inside a blocking stage_poll: with nothing waiting to be
+                                              launched they submit nothing before a batch completes, so the
+                                              newest batch's drains go out at once (a run's end) */
   int                       head;          /* oldest pending slot */
   int                       pending;       /* 0..FD_VS_DEPTH */
   vs_batch                  b[ FD_VS_DEPTH ];
@@ -671,7 +675,7 @@ vs_poller( fd_ed25519_gpu_stage_t * st ) {
       bool waiting = false;
       for( int j=0; j<st->pending && !waiting; j++ ) waiting = st->b[ (st->head + j) % FD_VS_DEPTH ].state == 1;
       if( !waiting ) {
-        int kr = fd_ed25519_gpu_frags_kick( st->ctx, st->kick == 1 );
+        int kr = fd_ed25519_gpu_frags_kick( st->ctx, st->kick == 3 || (st->kick == 1 && !st->poll_blocked) );
         if( kr ) r = kr;
       }
     }
@@ -755,8 +759,8 @@ fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc, 
   st->ctx = ctx; st->tc = tc; st->max_frags = max_frags;
   st->threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
   st->devparse = 1;
-  { char const * k = getenv( "FD_ED25519_GPU_STAGE_KICK" );         /* "0" off, "2" the newest batch's drains (A/Bs) */
-    st->kick = k && k[0] == '0' ? 0 : k && k[0] == '2' ? 2 : 1; }
+  { char const * k = getenv( "FD_ED25519_GPU_STAGE_KICK" );         /* "0" off, "2" newest, "3" oldest only (A/Bs) */
+    st->kick = k && (k[0] == '0' || k[0] == '2' || k[0] == '3') ? k[0] - '0' : 1; }
   char const * e = getenv( "FD_ED25519_GPU_STAGE_AUTOREG" );        /* "1": page-lock callers' frag areas */
   st->autoreg = e && e[0] == '1';
   memset( &st->stats, 0, sizeof(st->stats) );
@@ -862,7 +866,9 @@ fd_ed25519_gpu_stage_poll( fd_ed25519_gpu_stage_t * st, int block ) {
   vs_batch * b = &st->b[ st->head ];
   while( b->state != 4 && b->state != 5 ) {
     if( !block ) return FD_ED25519_GPU_PENDING;
+    st->poll_blocked++;
     st->cv.wait( lk );
+    st->poll_blocked--;
   }
   int err = b->state == 5 ? b->err : FD_ED25519_GPU_OK;
   b->state = 0;
