@@ -27,6 +27,7 @@
 #include <sys/mman.h>
 #include <unistd.h>
 #include <atomic>
+#include <chrono>
 #include <random>
 #include <thread>
 #include <vector>
@@ -59,10 +60,13 @@ static int stand_in_verify( uint8_t const * arena, uint64_t arena_sz, fd_ed25519
    arrays only at the poll that completes the batch, after a few PENDING
    answers to non-blocking polls -- the asynchronous discipline the stage's
    poller and replayer threads run against. */
-struct fq_ent { int8_t * status; uint64_t * tag; std::vector<int8_t> s; std::vector<uint64_t> t; int spins; };
+struct fq_ent { int8_t * status; uint64_t * tag; std::vector<int8_t> s; std::vector<uint64_t> t; int spins; uint64_t ready_ns; };
+static uint64_t stub_now( void ) {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>( std::chrono::steady_clock::now().time_since_epoch() ).count();
+}
 struct fd_ed25519_gpu {
   int8_t * pend_out; std::vector<int8_t> codes; int pend;
-  int devcap; fq_ent q[ FD_ED25519_GPU_QUEUE_DEPTH ]; int qh, qn; uint64_t submits, pending_polls, kicks;
+  int devcap; fq_ent q[ FD_ED25519_GPU_QUEUE_DEPTH ]; int qh, qn; uint64_t submits, pending_polls, kicks, kicks_newest, busy_ns;
 };
 
 extern "C" {
@@ -105,19 +109,19 @@ int fd_ed25519_gpu_frags_submit( fd_ed25519_gpu_t * ctx, uint8_t const * arena, 
   }
   for( uint64_t i=0; i<n; i++ )
     if( !e.s[ i ] ) e.s[ i ] = first[ i ] ? first[ i ] : (any_msg[ i ] ? (int8_t)FD_ED25519_ERR_MSG : (int8_t)FD_ED25519_SUCCESS);
-  e.status = status; e.tag = tag; e.spins = (int)(ctx->submits++ % 3u);
+  e.status = status; e.tag = tag; e.spins = (int)(ctx->submits++ % 3u); e.ready_ns = stub_now() + ctx->busy_ns;
   ctx->qn++;
   return FD_ED25519_GPU_OK;
 }
 int fd_ed25519_gpu_frags_poll( fd_ed25519_gpu_t * ctx, int block ) {
   if( !ctx->qn ) return FD_ED25519_GPU_OK;
   fq_ent & e = ctx->q[ ctx->qh ];
-  if( !block && e.spins > 0 ) { e.spins--; ctx->pending_polls++; return FD_ED25519_GPU_PENDING; }
+  if( !block && (e.spins > 0 || stub_now() < e.ready_ns) ) { if( e.spins > 0 ) e.spins--; ctx->pending_polls++; return FD_ED25519_GPU_PENDING; }
   for( size_t i=0; i<e.s.size(); i++ ) { e.status[ i ] = e.s[ i ]; e.tag[ i ] = e.t[ i ]; }
   ctx->qh = (ctx->qh + 1) % FD_ED25519_GPU_QUEUE_DEPTH; ctx->qn--;
   return FD_ED25519_GPU_OK;
 }
-int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t * ctx, int ) { ctx->kicks++; return FD_ED25519_GPU_OK; }
+int fd_ed25519_gpu_frags_kick( fd_ed25519_gpu_t * ctx, int oldest ) { ctx->kicks++; ctx->kicks_newest += !oldest; return FD_ED25519_GPU_OK; }
 int fd_ed25519_gpu_host_register_auto( fd_ed25519_gpu_t *, void *, uint64_t ) { return 1; }   /* "the caller's" */
 int fd_ed25519_gpu_host_unregister( fd_ed25519_gpu_t *, void * ) { return FD_ED25519_GPU_OK; }
 /* the shred path's GPU half: reads every byte the root kernel would (leaf,
@@ -257,6 +261,34 @@ static void check_stage_device_parse( int iters ) {
     if( !cd.submits || !cd.pending_polls ) { fprintf( stderr, "device-parse queue not exercised\n" ); exit( 1 ); }
     st_devp += cd.submits; st_kicks += cd.kicks;
     fd_ed25519_gpu_tcache_delete( td ); fd_ed25519_gpu_tcache_delete( th );
+  }
+}
+
+/* The run-end drain rule: a caller blocked in stage_poll with no batch left
+   to launch gets the newest batch's drains at once (kick in the newest mode);
+   a caller that polls without blocking keeps the oldest-batch kick.  The
+   stand-in device stays busy 5 ms per batch. */
+static void check_stage_run_end_drain( void ) {
+  for( int block=0; block<2; block++ ) {
+    fd_ed25519_gpu_t cd = {}; cd.devcap = 1; cd.busy_ns = 5000000u;
+    fd_ed25519_gpu_tcache_t * tc = fd_ed25519_gpu_tcache_new( 16, 64 );
+    fd_ed25519_gpu_stage_t * st = fd_ed25519_gpu_stage_new( &cd, tc, 64, 1 );
+    if( !st ) { fprintf( stderr, "stage_new\n" ); exit( 1 ); }
+    std::vector<uint8_t> a; std::vector<fd_ed25519_gpu_frag_t> fr;
+    for( int i=0; i<8; i++ ) rand_frag( a, fr );
+    exact ar( a );
+    std::vector<int8_t> res( fr.size() ); std::vector<uint64_t> sig( fr.size() );
+    if( fd_ed25519_gpu_stage_submit( st, ar.p, ar.n, fr.data(), fr.size(), res.data(), sig.data() ) ) { fprintf( stderr, "submit\n" ); exit( 1 ); }
+    int r;
+    while( (r = fd_ed25519_gpu_stage_poll( st, block )) == FD_ED25519_GPU_PENDING ) std::this_thread::yield();
+    if( r ) { fprintf( stderr, "poll %d\n", r ); exit( 1 ); }
+    fd_ed25519_gpu_stage_delete( st );
+    fd_ed25519_gpu_tcache_delete( tc );
+    if( block ? !cd.kicks_newest : (cd.kicks_newest != 0 || !cd.kicks) ) {
+      fprintf( stderr, "run-end drain rule: block %d, %lu kicks, %lu in the newest mode\n", block,
+               (unsigned long)cd.kicks, (unsigned long)cd.kicks_newest );
+      exit( 1 );
+    }
   }
 }
 
@@ -552,6 +584,7 @@ int main( int argc, char ** argv ) {
   check_frags( 3000 * scale );
   check_stage( 400 * scale );
   check_stage_device_parse( 200 * scale );
+  check_stage_run_end_drain();
   check_tcache( 20000 * scale );
   check_precompile( 3000 * scale );
   check_gossip( 3000 * scale );
