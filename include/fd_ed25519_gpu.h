@@ -400,7 +400,9 @@ int fd_ed25519_gpu_verify_frags( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t
    is given itself, keeping it registered until stage_delete (the area must
    then outlive the stage).  The stage owns ctx while it
    lives: no other call on ctx while batches are pending (the poller uses
-   it from its own thread). */
+   it from its own thread).  A blocking stage_poll with no batch left to
+   launch tells the stage no submit comes before a batch completes: the
+   pipelined batches' drain launches then go out at once (a burst's end). */
 typedef struct fd_ed25519_gpu_stage fd_ed25519_gpu_stage_t;
 
 fd_ed25519_gpu_stage_t * fd_ed25519_gpu_stage_new( fd_ed25519_gpu_t * ctx, fd_ed25519_gpu_tcache_t * tc,
